@@ -1,0 +1,741 @@
+/* fd_ed25519_oracle.c -- CPU restatement of the reference's Ed25519
+   verify path.  TEST INFRASTRUCTURE ONLY.
+
+   This file is the parity checker for the MI355X engine.  Only tests/,
+   __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it
+   (via oracle/liboracle.so).  The product library (firedancer_amd/)
+   never links or calls it.
+
+   Semantics restated: the AVX2 build of tinydancer-io/firedancer
+   (FD_HAS_AVX=1 => FD_ED25519_FE_IMPL 1, FD_ED25519_VERIFY_USE_2POINT 1),
+   which SURVEY.md section 0 identifies as the oracle.  Every
+   intermediate field element is bit-exact with the reference's limb
+   trajectory (the final compare is a memcmp of non-canonical
+   limbs 0..7, so the exact limb vectors matter, not just field values).
+
+   Pinning: tests/test_oracle.py checks this restatement against the
+   reference itself compiled from its own sources (oracle/Makefile ->
+   oracle/_ref/libfdref.so) on random, adversarial and golden corpora,
+   and against the committed golden fixtures under tests/golden/.
+
+   Integer model (why int32 limbs with wrapping are exact): the AVX path
+   keeps limbs in 64-bit lanes but every consumer of a limb that is not
+   a fresh column sum uses only its low 32 bits (_mm256_mul_epi32 takes
+   the low signed 32 bits, fd_avx_wl.h:136; swizzle-out stores the low
+   32 bits).  Adds/subs/permutes commute with truncation mod 2^32, so
+   int32 limbs with two's complement wrap reproduce the reference
+   exactly.  Column sums are exact int64; carries are floor shifts
+   (fd_avx_wl.h:205-208). */
+
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <pthread.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+typedef int32_t  i32;
+typedef int64_t  i64;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef uint8_t  u8;
+
+/* ---------------------------------------------------------------- */
+/* SHA-512 (FIPS 180-4).  Follows the streaming semantics of
+   src/ballet/sha512/fd_sha512.c:265-399 (init/append/fini); verify
+   hashes R || A || M in one message (fd_ed25519_user.c:411-413). */
+
+static u64 const sha512_k[80] = {
+  0x428a2f98d728ae22ULL,0x7137449123ef65cdULL,0xb5c0fbcfec4d3b2fULL,0xe9b5dba58189dbbcULL,0x3956c25bf348b538ULL,
+  0x59f111f1b605d019ULL,0x923f82a4af194f9bULL,0xab1c5ed5da6d8118ULL,0xd807aa98a3030242ULL,0x12835b0145706fbeULL,
+  0x243185be4ee4b28cULL,0x550c7dc3d5ffb4e2ULL,0x72be5d74f27b896fULL,0x80deb1fe3b1696b1ULL,0x9bdc06a725c71235ULL,
+  0xc19bf174cf692694ULL,0xe49b69c19ef14ad2ULL,0xefbe4786384f25e3ULL,0x0fc19dc68b8cd5b5ULL,0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL,0x4a7484aa6ea6e483ULL,0x5cb0a9dcbd41fbd4ULL,0x76f988da831153b5ULL,0x983e5152ee66dfabULL,
+  0xa831c66d2db43210ULL,0xb00327c898fb213fULL,0xbf597fc7beef0ee4ULL,0xc6e00bf33da88fc2ULL,0xd5a79147930aa725ULL,
+  0x06ca6351e003826fULL,0x142929670a0e6e70ULL,0x27b70a8546d22ffcULL,0x2e1b21385c26c926ULL,0x4d2c6dfc5ac42aedULL,
+  0x53380d139d95b3dfULL,0x650a73548baf63deULL,0x766a0abb3c77b2a8ULL,0x81c2c92e47edaee6ULL,0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL,0xa81a664bbc423001ULL,0xc24b8b70d0f89791ULL,0xc76c51a30654be30ULL,0xd192e819d6ef5218ULL,
+  0xd69906245565a910ULL,0xf40e35855771202aULL,0x106aa07032bbd1b8ULL,0x19a4c116b8d2d0c8ULL,0x1e376c085141ab53ULL,
+  0x2748774cdf8eeb99ULL,0x34b0bcb5e19b48a8ULL,0x391c0cb3c5c95a63ULL,0x4ed8aa4ae3418acbULL,0x5b9cca4f7763e373ULL,
+  0x682e6ff3d6b2b8a3ULL,0x748f82ee5defb2fcULL,0x78a5636f43172f60ULL,0x84c87814a1f0ab72ULL,0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL,0xa4506cebde82bde9ULL,0xbef9a3f7b2c67915ULL,0xc67178f2e372532bULL,0xca273eceea26619cULL,
+  0xd186b8c721c0c207ULL,0xeada7dd6cde0eb1eULL,0xf57d4f7fee6ed178ULL,0x06f067aa72176fbaULL,0x0a637dc5a2c898a6ULL,
+  0x113f9804bef90daeULL,0x1b710b35131c471bULL,0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,
+  0x431d67c49c100d4cULL,0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL
+};
+
+static inline u64 rotr64( u64 x, int n ) { return (x>>n) | (x<<(64-n)); }
+static inline u64 be64( u8 const * p ) {
+  u64 r = 0; for( int i=0; i<8; i++ ) r = (r<<8) | p[i]; return r;
+}
+
+static void sha512_block( u64 st[8], u8 const * blk ) {
+  u64 w[80];
+  for( int t=0; t<16; t++ ) w[t] = be64( blk + 8*t );
+  for( int t=16; t<80; t++ ) {
+    u64 s0 = rotr64(w[t-15],1) ^ rotr64(w[t-15],8) ^ (w[t-15]>>7);
+    u64 s1 = rotr64(w[t-2],19) ^ rotr64(w[t-2],61) ^ (w[t-2]>>6);
+    w[t] = w[t-16] + s0 + w[t-7] + s1;
+  }
+  u64 a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
+  for( int t=0; t<80; t++ ) {
+    u64 S1 = rotr64(e,14) ^ rotr64(e,18) ^ rotr64(e,41);
+    u64 ch = (e&f) ^ (~e&g);
+    u64 t1 = h + S1 + ch + sha512_k[t] + w[t];
+    u64 S0 = rotr64(a,28) ^ rotr64(a,34) ^ rotr64(a,39);
+    u64 mj = (a&b) ^ (a&c) ^ (b&c);
+    u64 t2 = S0 + mj;
+    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+t2;
+  }
+  st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
+}
+
+/* Hash the concatenation of up to 3 byte strings. */
+static void sha512_3( u8 out[64], u8 const * p0, u64 n0, u8 const * p1, u64 n1, u8 const * p2, u64 n2 ) {
+  u64 st[8] = { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL };
+  u8 buf[128]; u64 used = 0;
+  u8 const * ps[3] = { p0, p1, p2 }; u64 ns[3] = { n0, n1, n2 };
+  u64 total = n0 + n1 + n2;
+  for( int s=0; s<3; s++ ) {
+    u8 const * p = ps[s]; u64 n = ns[s];
+    while( n ) {
+      u64 take = 128 - used; if( take > n ) take = n;
+      memcpy( buf+used, p, take ); used += take; p += take; n -= take;
+      if( used==128 ) { sha512_block( st, buf ); used = 0; }
+    }
+  }
+  buf[used++] = 0x80;
+  if( used > 112 ) { memset( buf+used, 0, 128-used ); sha512_block( st, buf ); used = 0; }
+  memset( buf+used, 0, 112-used );
+  u64 bits_hi = total >> 61, bits_lo = total << 3;
+  for( int i=0; i<8; i++ ) { buf[112+i] = (u8)(bits_hi >> (56-8*i)); buf[120+i] = (u8)(bits_lo >> (56-8*i)); }
+  sha512_block( st, buf );
+  for( int i=0; i<8; i++ ) for( int j=0; j<8; j++ ) out[8*i+j] = (u8)(st[i] >> (56-8*j));
+}
+
+EXPORT void oracle_sha512( u8 const * msg, u64 sz, u8 * out ) { sha512_3( out, msg, sz, NULL, 0, NULL, 0 ); }
+
+/* ---------------------------------------------------------------- */
+/* Scalar reduction mod L = 2^252 + 27742317777372353535851937790883648493.
+   Restates fd_ed25519_sc_reduce (fd_ed25519_user.c:3-110): the ref10
+   signed 21-bit limb schedule.  The schedule's output is the canonical
+   residue in [0,L); the test suite checks this restatement byte-exact
+   against the reference on random and edge inputs. */
+
+static inline i64 ld21( u8 const * s, int bit ) {
+  /* 21 bits starting at 'bit' (little endian) */
+  u64 v = 0;
+  int byte = bit >> 3;
+  for( int i=0; i<4 && byte+i<64; i++ ) v |= ((u64)s[byte+i]) << (8*i);
+  return (i64)((v >> (bit & 7)) & 0x1fffff);
+}
+
+#define SC_FOLD(x,k) do { s[(k)-12] += (x)*666643; s[(k)-11] += (x)*470296; s[(k)-10] += (x)*654183; \
+                          s[(k)-9]  -= (x)*997805; s[(k)-8]  += (x)*136657; s[(k)-7]  -= (x)*683901; (x) = 0; } while(0)
+#define SC_CARRY_R(k) do { i64 c = (s[k] + (1LL<<20)) >> 21; s[(k)+1] += c; s[k] -= (i64)((u64)c << 21); } while(0)
+#define SC_CARRY_F(k) do { i64 c = s[k] >> 21;               s[(k)+1] += c; s[k] -= (i64)((u64)c << 21); } while(0)
+
+EXPORT void oracle_sc_reduce( u8 const * in, u8 * out ) {
+  i64 s[24];
+  for( int i=0; i<23; i++ ) s[i] = ld21( in, 21*i );
+  /* top limb: bits 483..511 (29 bits) */
+  { u64 t = 0; for( int i=0; i<8; i++ ) t |= ((u64)in[56+i]) << (8*i); s[23] = (i64)(t >> 35); }
+
+  for( int k=23; k>=18; k-- ) SC_FOLD( s[k], k );
+  SC_CARRY_R(6); SC_CARRY_R(8); SC_CARRY_R(10); SC_CARRY_R(12); SC_CARRY_R(14); SC_CARRY_R(16);
+  SC_CARRY_R(7); SC_CARRY_R(9); SC_CARRY_R(11); SC_CARRY_R(13); SC_CARRY_R(15);
+  for( int k=17; k>=12; k-- ) SC_FOLD( s[k], k );
+  SC_CARRY_R(0); SC_CARRY_R(2); SC_CARRY_R(4); SC_CARRY_R(6); SC_CARRY_R(8); SC_CARRY_R(10);
+  SC_CARRY_R(1); SC_CARRY_R(3); SC_CARRY_R(5); SC_CARRY_R(7); SC_CARRY_R(9); SC_CARRY_R(11);
+  SC_FOLD( s[12], 12 );
+  for( int k=0; k<12; k++ ) SC_CARRY_F(k);
+  SC_FOLD( s[12], 12 );
+  for( int k=0; k<11; k++ ) SC_CARRY_F(k);
+
+  /* pack 12 x 21 bits little endian */
+  memset( out, 0, 32 );
+  for( int k=0; k<12; k++ ) {
+    u64 v = (u64)s[k];
+    for( int b=0; b<21; b++ ) {
+      int bit = 21*k + b;
+      if( bit >= 256 ) break;
+      if( (v>>b) & 1 ) out[bit>>3] |= (u8)(1u << (bit&7));
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- */
+/* Field arithmetic GF(2^255-19): 10 signed limbs, radix 2^25.5
+   (26,25,26,25,...).  fe[k] is an int32. */
+
+typedef struct { i32 v[10]; } fe;
+
+static inline u32 ld3( u8 const * s ) { return (u32)s[0] | ((u32)s[1]<<8) | ((u32)s[2]<<16); }
+static inline u32 ld4( u8 const * s ) { return ld3(s) | ((u32)s[3]<<24); }
+
+/* Carry helpers: c = h + 2^(w-1); next += c >> w; h -= c & ~(2^w-1)
+   (the m38u/m39u mask form of fd_ed25519_fe.c). */
+#define CARRY26(h,n) do { i64 c_ = (h) + (1LL<<25); (n) += c_ >> 26; (h) -= c_ & ~((1LL<<26)-1); } while(0)
+#define CARRY25(h,n) do { i64 c_ = (h) + (1LL<<24); (n) += c_ >> 25; (h) -= c_ & ~((1LL<<25)-1); } while(0)
+#define CARRY25_19(h,n) do { i64 c_ = (h) + (1LL<<24); (n) += (c_ >> 25)*19; (h) -= c_ & ~((1LL<<25)-1); } while(0)
+
+/* fe_frombytes (avx/fd_ed25519_fe.c:4-46): lax load, bit 255 ignored,
+   y >= p NOT rejected. */
+static void fe_frombytes( fe * h, u8 const * s ) {
+  i64 h0 = (i64)ld4( s      );
+  i64 h1 = (i64)ld3( s +  4 ) << 6;
+  i64 h2 = (i64)ld3( s +  7 ) << 5;
+  i64 h3 = (i64)ld3( s + 10 ) << 3;
+  i64 h4 = (i64)ld3( s + 13 ) << 2;
+  i64 h5 = (i64)ld4( s + 16 );
+  i64 h6 = (i64)ld3( s + 20 ) << 7;
+  i64 h7 = (i64)ld3( s + 23 ) << 5;
+  i64 h8 = (i64)ld3( s + 26 ) << 4;
+  i64 h9 = (i64)(ld3( s + 29 ) & 0x7fffffu) << 2;
+  CARRY25_19( h9, h0 ); CARRY25( h1, h2 ); CARRY25( h3, h4 ); CARRY25( h5, h6 ); CARRY25( h7, h8 );
+  CARRY26( h0, h1 ); CARRY26( h2, h3 ); CARRY26( h4, h5 ); CARRY26( h6, h7 ); CARRY26( h8, h9 );
+  h->v[0]=(i32)h0; h->v[1]=(i32)h1; h->v[2]=(i32)h2; h->v[3]=(i32)h3; h->v[4]=(i32)h4;
+  h->v[5]=(i32)h5; h->v[6]=(i32)h6; h->v[7]=(i32)h7; h->v[8]=(i32)h8; h->v[9]=(i32)h9;
+}
+
+/* fe_tobytes (avx/fd_ed25519_fe.c:48-110): canonical encoding.  All
+   arithmetic in int32 as the reference does. */
+static void fe_tobytes( u8 * s, fe const * f ) {
+  i32 h[10]; for( int i=0; i<10; i++ ) h[i] = f->v[i];
+  i32 q = (i32)((u32)(19*h[9]) + (1u<<24)) >> 25;
+  for( int i=0; i<10; i++ ) q = (h[i] + q) >> ((i&1) ? 25 : 26);
+  h[0] += 19*q;
+  for( int i=0; i<9; i++ ) {
+    int w = (i&1) ? 25 : 26;
+    h[i+1] += h[i] >> w;
+    h[i] &= (i32)((1u<<w)-1u);
+  }
+  h[9] &= (i32)((1u<<25)-1u);
+  u64 w0 = ((u64)(u32)h[0]) | ((u64)(u32)h[1]<<26) | ((u64)(u32)h[2]<<51);
+  u64 w1 = ((u64)(u32)h[2]>>13) | ((u64)(u32)h[3]<<13) | ((u64)(u32)h[4]<<38);
+  u64 w2 = ((u64)(u32)h[5]) | ((u64)(u32)h[6]<<25) | ((u64)(u32)h[7]<<51);
+  u64 w3 = ((u64)(u32)h[7]>>13) | ((u64)(u32)h[8]<<12) | ((u64)(u32)h[9]<<38);
+  u64 ws[4] = { w0, w1, w2, w3 };
+  for( int i=0; i<4; i++ ) for( int j=0; j<8; j++ ) s[8*i+j] = (u8)(ws[i] >> (8*j));
+}
+
+static int fe_isnonzero( fe const * f ) { u8 s[32]; fe_tobytes( s, f ); u8 a = 0; for( int i=0; i<32; i++ ) a |= s[i]; return a!=0; }
+static int fe_isnegative( fe const * f ) { u8 s[32]; fe_tobytes( s, f ); return s[0] & 1; }
+
+static inline void fe_add( fe * h, fe const * f, fe const * g ) { for( int i=0; i<10; i++ ) h->v[i] = (i32)((u32)f->v[i] + (u32)g->v[i]); }
+static inline void fe_sub( fe * h, fe const * f, fe const * g ) { for( int i=0; i<10; i++ ) h->v[i] = (i32)((u32)f->v[i] - (u32)g->v[i]); }
+static inline void fe_neg( fe * h, fe const * f )               { for( int i=0; i<10; i++ ) h->v[i] = (i32)(0u - (u32)f->v[i]); }
+static inline void fe_set( fe * h, i32 x )                      { memset( h, 0, sizeof(fe) ); h->v[0] = x; }
+
+/* The shared reduction: the 12-step carry chain
+   0,4,1,5,2,6,3,7,4,8,9,0 (fd_ed25519_fe_avx_inl.h:164-175 and
+   avx/fd_ed25519_fe.c:242-283). */
+static inline void fe_carry( fe * out, i64 h[10] ) {
+  CARRY26( h[0], h[1] ); CARRY26( h[4], h[5] );
+  CARRY25( h[1], h[2] ); CARRY25( h[5], h[6] );
+  CARRY26( h[2], h[3] ); CARRY26( h[6], h[7] );
+  CARRY25( h[3], h[4] ); CARRY25( h[7], h[8] );
+  CARRY26( h[4], h[5] ); CARRY26( h[8], h[9] );
+  CARRY25_19( h[9], h[0] );
+  CARRY26( h[0], h[1] );
+  for( int i=0; i<10; i++ ) out->v[i] = (i32)h[i];
+}
+
+/* Column sums of f*g mod 2^255-19 from int64 operand vectors:
+   h[k] = sum_{i+j=k} c_ij f_i g_j + 19 sum_{i+j=k+10} c_ij f_i g_j,
+   c_ij = 2 when i and j are both odd.  ff/gg carry the already-scaled
+   operands so both the AVX (int32-wrapped) and scalar (int64) operand
+   conventions can be expressed. */
+
+/* AVX multiply (FE_AVX_INL_MUL, fd_ed25519_fe_avx_inl.h:484-590):
+   g*19 and 2*f are formed and then consumed as low-32-bit signed
+   operands of _mm256_mul_epi32. */
+static void fe_mul_avx( fe * h, fe const * f, fe const * g ) {
+  i64 F[10], G[10], F2[10], G19[10];
+  for( int i=0; i<10; i++ ) {
+    F[i]   = (i64)f->v[i];
+    G[i]   = (i64)g->v[i];
+    F2[i]  = (i64)(i32)(2u  * (u32)f->v[i]);
+    G19[i] = (i64)(i32)(19u * (u32)g->v[i]);
+  }
+  i64 s[10];
+  for( int k=0; k<10; k++ ) s[k] = 0;
+  for( int i=0; i<10; i++ ) for( int j=0; j<10; j++ ) {
+    int both_odd = (i&1) & (j&1);
+    i64 a = both_odd ? F2[i] : F[i];
+    if( i+j < 10 ) s[i+j]    += a * G[j];
+    else           s[i+j-10] += a * G19[j];
+  }
+  fe_carry( h, s );
+}
+
+/* Scalar multiply (avx/fd_ed25519_fe.c:112-291): 19*g and 2*f formed in
+   int64 (no wrap).  Used by fd_ed25519_fe_mul call sites (sqrtm1 fixup
+   in frombytes_vartime_2 and is_identity). */
+static void fe_mul_scalar( fe * h, fe const * f, fe const * g ) {
+  i64 s[10];
+  for( int k=0; k<10; k++ ) s[k] = 0;
+  for( int i=0; i<10; i++ ) for( int j=0; j<10; j++ ) {
+    i64 a = (i64)f->v[i] * (((i&1)&(j&1)) ? 2 : 1);
+    i64 b = (i64)g->v[j] * ((i+j>=10) ? 19 : 1);
+    if( i+j < 10 ) s[i+j] += a*b; else s[i+j-10] += a*b;
+  }
+  fe_carry( h, s );
+}
+
+/* AVX square with per-lane scale n in {1,2} (FE_AVX_INL_SQN,
+   fd_ed25519_fe_avx_inl.h:592-677): operands 2*f, 19*f, 38*f are each
+   consumed as low-32-bit signed values; column sums are doubled when
+   n==2 before the carry chain. */
+static void fe_sqn_avx( fe * h, fe const * f, int n ) {
+  i64 F[10], F2[10], F19[10], F38[10];
+  for( int i=0; i<10; i++ ) {
+    F[i]   = (i64)f->v[i];
+    F2[i]  = (i64)(i32)(2u  * (u32)f->v[i]);
+    F19[i] = (i64)(i32)(19u * (u32)f->v[i]);
+    F38[i] = (i64)(i32)(38u * (u32)f->v[i]);
+  }
+  /* The reference's product terms (one per unordered pair):
+       diagonal i==j: f_i * f_i * (odd?2:1) * (i>=5? 19:1)
+                       realised as f_i*f_i, f_i*F2..., see below.
+     We enumerate exactly the operand pairs the macro uses. */
+#define P(a,b) ((i64)(a) * (i64)(b))
+  i64 s[10];
+  s[0] = P(F[0],F[0])  + P(F2[1],F38[9]) + P(F2[2],F19[8]) + P(F2[3],F38[7]) + P(F2[4],F19[6]) + P(F[5],F38[5]);
+  s[1] = P(F2[0],F[1]) + P(F[2],F38[9])  + P(F2[3],F19[8]) + P(F[4],F38[7])  + P(F2[5],F19[6]);
+  s[2] = P(F2[0],F[2]) + P(F2[1],F[1])   + P(F2[3],F38[9]) + P(F2[4],F19[8]) + P(F2[5],F38[7]) + P(F[6],F19[6]);
+  s[3] = P(F2[0],F[3]) + P(F2[1],F[2])   + P(F[4],F38[9])  + P(F2[5],F19[8]) + P(F[6],F38[7]);
+  s[4] = P(F2[0],F[4]) + P(F2[1],F2[3])  + P(F[2],F[2])    + P(F2[5],F38[9]) + P(F2[6],F19[8]) + P(F[7],F38[7]);
+  s[5] = P(F2[0],F[5]) + P(F2[1],F[4])   + P(F2[2],F[3])   + P(F[6],F38[9])  + P(F2[7],F19[8]);
+  s[6] = P(F2[0],F[6]) + P(F2[1],F2[5])  + P(F2[2],F[4])   + P(F2[3],F[3])   + P(F2[7],F38[9]) + P(F[8],F19[8]);
+  s[7] = P(F2[0],F[7]) + P(F2[1],F[6])   + P(F2[2],F[5])   + P(F2[3],F[4])   + P(F[8],F38[9]);
+  s[8] = P(F2[0],F[8]) + P(F2[1],F2[7])  + P(F2[2],F[6])   + P(F2[3],F2[5])  + P(F[4],F[4])    + P(F[9],F38[9]);
+  s[9] = P(F2[0],F[9]) + P(F2[1],F[8])   + P(F2[2],F[7])   + P(F2[3],F[6])   + P(F2[4],F[5]);
+#undef P
+  if( n==2 ) for( int k=0; k<10; k++ ) s[k] += s[k];
+  fe_carry( h, s );
+}
+
+static inline void fe_sq_avx( fe * h, fe const * f ) { fe_sqn_avx( h, f, 1 ); }
+
+/* ---------------------------------------------------------------- */
+/* 4-lane vectors of field elements: the AVX path's wl_t x10 state. */
+
+typedef struct { fe l[4]; } fe4;
+
+#include "fd_ed25519_oracle_tables.h"
+
+static inline void v_perm( fe4 * h, fe4 const * f, int a, int b, int c, int d ) {
+  fe4 t; t.l[0]=f->l[a]; t.l[1]=f->l[b]; t.l[2]=f->l[c]; t.l[3]=f->l[d]; *h = t;
+}
+static inline void v_mul( fe4 * h, fe4 const * f, fe4 const * g ) {
+  fe4 t; for( int i=0; i<4; i++ ) fe_mul_avx( &t.l[i], &f->l[i], &g->l[i] ); *h = t;
+}
+static inline void v_sqn( fe4 * h, fe4 const * f, int n0, int n1, int n2, int n3 ) {
+  int n[4] = { n0, n1, n2, n3 };
+  fe4 t; for( int i=0; i<4; i++ ) fe_sqn_avx( &t.l[i], &f->l[i], n[i] ); *h = t;
+}
+/* wl_dbl_mix (fd_ed25519_fe_avx.h:35-44) as computed: [a-b-c, b+c, b-c, d-b+c] */
+static inline void v_dbl_mix( fe4 * h, fe4 const * f ) {
+  fe4 t;
+  for( int k=0; k<10; k++ ) {
+    u32 a=(u32)f->l[0].v[k], b=(u32)f->l[1].v[k], c=(u32)f->l[2].v[k], d=(u32)f->l[3].v[k];
+    t.l[0].v[k]=(i32)(a-b-c); t.l[1].v[k]=(i32)(b+c); t.l[2].v[k]=(i32)(b-c); t.l[3].v[k]=(i32)(d-b+c);
+  }
+  *h = t;
+}
+/* wl_sub_mix (fd_ed25519_fe_avx.h:49-57): [c-b, c+b, 2a-d, 2a+d] */
+static inline void v_sub_mix( fe4 * h, fe4 const * f ) {
+  fe4 t;
+  for( int k=0; k<10; k++ ) {
+    u32 a=(u32)f->l[0].v[k], b=(u32)f->l[1].v[k], c=(u32)f->l[2].v[k], d=(u32)f->l[3].v[k];
+    t.l[0].v[k]=(i32)(c-b); t.l[1].v[k]=(i32)(c+b); t.l[2].v[k]=(i32)(2*a-d); t.l[3].v[k]=(i32)(2*a+d);
+  }
+  *h = t;
+}
+/* wl_subadd_12 (fd_ed25519_fe_avx.h:62-69): [a, b-c, b+c, d] */
+static inline void v_subadd_12( fe4 * h, fe4 const * f ) {
+  fe4 t;
+  for( int k=0; k<10; k++ ) {
+    u32 a=(u32)f->l[0].v[k], b=(u32)f->l[1].v[k], c=(u32)f->l[2].v[k], d=(u32)f->l[3].v[k];
+    t.l[0].v[k]=(i32)a; t.l[1].v[k]=(i32)(b-c); t.l[2].v[k]=(i32)(b+c); t.l[3].v[k]=(i32)d;
+  }
+  *h = t;
+}
+
+/* ---------------------------------------------------------------- */
+/* Group operations. */
+
+typedef struct { fe X, Y, Z, T; } ge_p3;
+typedef struct { fe X, Y, Z; } ge_p2;
+
+/* fe_avx_pow22523 (avx/fd_ed25519_fe_avx.h:246-275), per lane. */
+static void fe_pow22523_avx( fe * out, fe const * f ) {
+  fe t0, t1, t2;
+#define SQI(d,s,n) do { fe_sq_avx( (d), (s) ); for( int i_=1; i_<(n); i_++ ) fe_sq_avx( (d), (d) ); } while(0)
+  fe_sq_avx( &t0, f );
+  SQI( &t1, &t0, 2 );
+  fe_mul_avx( &t1, f, &t1 );
+  fe_mul_avx( &t0, &t0, &t1 );
+  fe_sq_avx( &t0, &t0 );
+  fe_mul_avx( &t0, &t1, &t0 );
+  SQI( &t1, &t0, 5 );
+  fe_mul_avx( &t0, &t1, &t0 );
+  SQI( &t1, &t0, 10 );
+  fe_mul_avx( &t1, &t1, &t0 );
+  SQI( &t2, &t1, 20 );
+  fe_mul_avx( &t1, &t2, &t1 );
+  SQI( &t1, &t1, 10 );
+  fe_mul_avx( &t0, &t1, &t0 );
+  SQI( &t1, &t0, 50 );
+  fe_mul_avx( &t1, &t1, &t0 );
+  SQI( &t2, &t1, 100 );
+  fe_mul_avx( &t1, &t2, &t1 );
+  SQI( &t1, &t1, 50 );
+  fe_mul_avx( &t0, &t1, &t0 );
+  SQI( &t0, &t0, 2 );
+  fe_mul_avx( out, &t0, f );
+#undef SQI
+}
+
+/* One point of fd_ed25519_ge_frombytes_vartime_2
+   (avx/fd_ed25519_ge.c:222-299).  The two lanes of the reference are
+   independent, so each point is decompressed on its own with the same
+   per-lane operation sequence.  Returns 0 or -2 (ERR_PUBKEY). */
+static int ge_frombytes_lane( ge_p3 * h, u8 const * s ) {
+  fe y, u, v, w, x, vxx, check;
+  fe_frombytes( &y, s );
+  fe_sq_avx( &u, &y );
+  fe_mul_avx( &v, &u, &FD_ORACLE_D );
+  u.v[0] -= 1;                                 /* u = y^2-1 */
+  v.v[0] += 1;                                 /* v = dy^2+1 */
+  fe_sq_avx( &w, &v );
+  fe_mul_avx( &w, &w, &v );                    /* w = v^3 */
+  fe_sq_avx( &x, &w );
+  fe_mul_avx( &x, &x, &v );
+  fe_mul_avx( &x, &x, &u );                    /* uv^7 */
+  fe_pow22523_avx( &x, &x );
+  fe_mul_avx( &x, &x, &w );
+  fe_mul_avx( &x, &x, &u );                    /* uv^3 (uv^7)^((p-5)/8) */
+  fe_sq_avx( &vxx, &x );
+  fe_mul_avx( &vxx, &vxx, &v );
+  fe_sub( &check, &vxx, &u );
+  if( fe_isnonzero( &check ) ) {
+    fe_add( &check, &vxx, &u );
+    if( fe_isnonzero( &check ) ) return -2;
+    fe_mul_scalar( &x, &x, &FD_ORACLE_SQRTM1 );
+  }
+  if( fe_isnegative( &x ) != (s[31] >> 7) ) fe_neg( &x, &x );
+  h->X = x; h->Y = y; fe_set( &h->Z, 1 );
+  fe_mul_avx( &h->T, &h->X, &h->Y );
+  return 0;
+}
+
+/* fd_ed25519_ge_p2_dbl (avx/fd_ed25519_ge.c:127-141) into p1p1 (X,Y,Z,T). */
+static void ge_p2_dbl( fe r[4], fe const * X, fe const * Y, fe const * Z ) {
+  fe t0;
+  fe_add( &r[1], X, Y );
+  fe tmpY = r[1];
+  fe_sqn_avx( &r[0], X, 1 );
+  fe_sqn_avx( &r[2], Y, 1 );
+  fe_sqn_avx( &r[3], Z, 2 );
+  fe_sqn_avx( &t0, &tmpY, 1 );
+  fe_add( &r[1], &r[2], &r[0] );
+  fe_sub( &r[2], &r[2], &r[0] );
+  fe_sub( &r[0], &t0, &r[1] );
+  fe_sub( &r[3], &r[3], &r[2] );
+}
+
+/* fd_ed25519_ge_p3_is_small_order (fd_ed25519_ge.c:61-66): [8]P via
+   three doublings, then limb-equality identity test. */
+static int ge_is_small_order( ge_p3 const * p ) {
+  fe X = p->X, Y = p->Y, Z = p->Z;
+  fe r[4];
+  for( int i=0; i<2; i++ ) {
+    ge_p2_dbl( r, &X, &Y, &Z );
+    fe_mul_avx( &X, &r[0], &r[3] ); fe_mul_avx( &Y, &r[1], &r[2] ); fe_mul_avx( &Z, &r[2], &r[3] );
+  }
+  ge_p2_dbl( r, &X, &Y, &Z );
+  ge_p3 t;
+  fe_mul_avx( &t.X, &r[0], &r[3] ); fe_mul_avx( &t.Y, &r[1], &r[2] );
+  fe_mul_avx( &t.Z, &r[2], &r[3] ); fe_mul_avx( &t.T, &r[0], &r[1] );
+  fe one, zero, c0, c1; fe_set( &one, 1 ); fe_set( &zero, 0 );
+  fe_mul_scalar( &c0, &t.X, &one ); fe_mul_scalar( &c1, &zero, &t.Z );
+  int x = !memcmp( c0.v, c1.v, sizeof(c0.v) );
+  fe_mul_scalar( &c0, &t.Y, &one ); fe_mul_scalar( &c1, &one, &t.Z );
+  int y = !memcmp( c0.v, c1.v, sizeof(c0.v) );
+  return x & y;
+}
+
+/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400): signed sliding
+   window recoding, digits odd in [-15,15]. */
+static void ge_slide( signed char * r, u8 const * a ) {
+  for( int i=0; i<256; i++ ) r[i] = (signed char)(1 & (a[i>>3] >> (i&7)));
+  for( int i=0; i<256; i++ ) {
+    if( !r[i] ) continue;
+    for( int b=1; b<=6 && i+b<256; b++ ) {
+      if( !r[i+b] ) continue;
+      int up = r[i+b] << b;
+      if( r[i] + up <= 15 ) { r[i] = (signed char)(r[i] + up); r[i+b] = 0; }
+      else if( r[i] - up >= -15 ) {
+        r[i] = (signed char)(r[i] - up);
+        for( int k=i+b; k<256; k++ ) { if( !r[k] ) { r[k] = 1; break; } r[k] = 0; }
+      } else break;
+    }
+  }
+}
+
+/* fd_ed25519_ge_double_scalarmult_vartime, inlined AVX variant
+   (avx/fd_ed25519_ge.c:408-527): r = [a]A + [b]B with A already
+   negated by the caller. */
+static void ge_dsm( ge_p2 * out, u8 const * a, ge_p3 const * A, u8 const * b ) {
+  signed char as[256], bs[256];
+  ge_slide( as, a ); ge_slide( bs, b );
+
+  fe4 Ai[8];
+  fe4 vr, vt, vu;
+  fe4 const * d111 = &FD_ORACLE_V111D2;
+  vr.l[0] = A->Z; vr.l[1] = A->Y; vr.l[2] = A->X; vr.l[3] = A->T;
+  v_mul( &vu, &vr, d111 ); v_subadd_12( &vu, &vu ); Ai[0] = vu;
+  v_perm( &vt, &vr, 2,1,2,0 );
+  v_perm( &vr, &vr, 1,0,3,2 );
+  fe_set( &vr.l[1], 0 ); fe_set( &vr.l[2], 0 ); fe_set( &vr.l[3], 0 );
+  for( int l=0; l<4; l++ ) fe_add( &vt.l[l], &vt.l[l], &vr.l[l] );
+  v_sqn( &vt, &vt, 1,1,1,2 );
+  v_dbl_mix( &vt, &vt );
+  v_perm( &vr, &vt, 2,1,0,0 );
+  v_perm( &vt, &vt, 3,2,3,1 );
+  v_mul( &vr, &vt, &vr );
+  v_subadd_12( &vr, &vr );
+  for( int i=0; i<7; i++ ) {
+    v_mul( &vt, &vr, &vu );
+    v_sub_mix( &vt, &vt );
+    v_perm( &vu, &vt, 3,1,0,0 );
+    v_perm( &vt, &vt, 2,3,2,1 );
+    v_mul( &vt, &vt, &vu );
+    v_mul( &vu, &vt, d111 ); v_subadd_12( &vu, &vu ); Ai[i+1] = vu;
+  }
+
+  memset( &vr, 0, sizeof(vr) );
+  vr.l[1].v[0] = 1; vr.l[2].v[0] = 1;
+  int i;
+  for( i=255; i>=0; i-- ) if( as[i] || bs[i] ) break;
+  for( ; i>=0; i-- ) {
+    v_perm( &vt, &vr, 0,1,0,2 );
+    v_perm( &vu, &vr, 1,0,3,2 );
+    fe_set( &vu.l[1], 0 ); fe_set( &vu.l[2], 0 ); fe_set( &vu.l[3], 0 );
+    for( int l=0; l<4; l++ ) fe_add( &vt.l[l], &vt.l[l], &vu.l[l] );
+    v_sqn( &vt, &vt, 1,1,1,2 );
+    v_dbl_mix( &vt, &vt );
+    for( int j=0; j<2; j++ ) {
+      int sl = j ? bs[i] : as[i];
+      if( !sl ) continue;
+      fe4 const * tab = j ? FD_ORACLE_BI_PRECOMP : Ai;
+      v_perm( &vu, &vt, 2,1,0,0 );
+      v_perm( &vt, &vt, 3,2,3,1 );
+      v_mul( &vt, &vu, &vt );
+      vu = tab[ (sl<0 ? -sl : sl) >> 1 ];
+      if( sl<0 ) v_perm( &vu, &vu, 0,2,1,3 );
+      v_subadd_12( &vt, &vt );
+      v_mul( &vt, &vt, &vu );
+      v_sub_mix( &vt, &vt );
+      if( !(sl<0) ) v_perm( &vt, &vt, 0,1,3,2 );
+    }
+    v_perm( &vr, &vt, 3,2,3,3 );
+    /* lane 3 of vr is never consumed (p2 has three coordinates) */
+    v_mul( &vr, &vt, &vr );
+  }
+  out->X = vr.l[0]; out->Y = vr.l[1]; out->Z = vr.l[2];
+}
+
+/* fd_ed25519_verify, AVX2 build (fd_ed25519_user.c:346-433). */
+EXPORT int oracle_verify( void const * msg, u64 sz, void const * sig, void const * pub ) {
+  u8 const * r = (u8 const *)sig;
+  u8 const * s = r + 32;
+
+  /* S range check (fd_ed25519_user.c:372-393), incl. the early
+     SUCCESS at :379. */
+  if( s[31] > 0x10 ) return -1;
+  if( s[31]==0x10 ) {
+    int nz = 0; for( int i=16; i<31; i++ ) nz |= s[i];
+    if( nz ) return 0;
+    static u8 const l_low[16] = { 0xED,0xD3,0xF5,0x5C,0x1A,0x63,0x12,0x58,0xD6,0x9C,0xF7,0xA2,0xDE,0xF9,0xDE,0x14 };
+    int i;
+    for( i=15; i>=0; i-- ) {
+      if( s[i] < l_low[i] ) break;
+      if( s[i] > l_low[i] ) return -1;
+    }
+    if( i<0 ) return -1;
+  }
+
+  ge_p3 A, Rd;
+  if( ge_frombytes_lane( &A,  (u8 const *)pub ) ) return -2;
+  if( ge_frombytes_lane( &Rd, r ) )               return -2;
+  if( ge_is_small_order( &A  ) ) return -2;
+  if( ge_is_small_order( &Rd ) ) return -1;
+
+  fe_neg( &A.X, &A.X );
+  fe_neg( &A.T, &A.T );
+
+  u8 h[64];
+  sha512_3( h, r, 32, (u8 const *)pub, 32, (u8 const *)msg, sz );
+  oracle_sc_reduce( h, h );
+
+  ge_p2 R;
+  ge_dsm( &R, h, &A, s );
+
+  fe xz, yz;
+  fe_mul_avx( &xz, &R.Z, &Rd.X );
+  fe_mul_avx( &yz, &R.Z, &Rd.Y );
+  /* memcmp of the first 32 bytes of fd_ed25519_fe_t = limbs 0..7 */
+  return ( memcmp( xz.v, R.X.v, 32 ) | memcmp( yz.v, R.Y.v, 32 ) ) ? -3 : 0;
+}
+
+/* ---------------------------------------------------------------- */
+/* Internals exported for differential tests against the reference. */
+
+EXPORT void oracle_fe_mul_avx( i32 * h, i32 const * f, i32 const * g ) { fe_mul_avx( (fe *)h, (fe const *)f, (fe const *)g ); }
+EXPORT void oracle_fe_mul_scalar( i32 * h, i32 const * f, i32 const * g ) { fe_mul_scalar( (fe *)h, (fe const *)f, (fe const *)g ); }
+EXPORT void oracle_fe_sqn_avx( i32 * h, i32 const * f, int n ) { fe_sqn_avx( (fe *)h, (fe const *)f, n ); }
+EXPORT void oracle_fe_frombytes( i32 * h, u8 const * s ) { fe_frombytes( (fe *)h, s ); }
+EXPORT void oracle_fe_tobytes( u8 * s, i32 const * h ) { fe_tobytes( s, (fe const *)h ); }
+EXPORT void oracle_ge_slide( signed char * r, u8 const * a ) { ge_slide( r, a ); }
+/* decompress one point: out = X,Y,Z,T limbs (40 int32); returns 0/-2 */
+EXPORT int oracle_ge_frombytes( i32 * out, u8 const * s ) { return ge_frombytes_lane( (ge_p3 *)out, s ); }
+EXPORT int oracle_ge_is_small_order( i32 const * p ) { return ge_is_small_order( (ge_p3 const *)p ); }
+/* out = X,Y,Z (30 int32) of [a](A) + [b]B where A is given as 40 int32 */
+EXPORT void oracle_ge_dsm( i32 * out, u8 const * a, i32 const * A, u8 const * b ) { ge_dsm( (ge_p2 *)out, a, (ge_p3 const *)A, b ); }
+
+/* Batch verify over the packed corpus layout used by the engine and the
+   tests: sig[i*64], pub[i*32], msg at data+msg_off[i], msg_sz[i]. */
+typedef struct {
+  u64 n; u8 const * sig; u8 const * pub; u8 const * data; u64 const * msg_off; u32 const * msg_sz; i32 * out;
+  u64 lo, hi;
+} batch_job_t;
+
+static void * batch_worker( void * arg ) {
+  batch_job_t * j = (batch_job_t *)arg;
+  for( u64 i=j->lo; i<j->hi; i++ )
+    j->out[i] = oracle_verify( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i );
+  return NULL;
+}
+
+EXPORT void oracle_verify_batch( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
+                                 u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
+  if( nthreads < 1 ) nthreads = 1;
+  if( nthreads > 256 ) nthreads = 256;
+  pthread_t th[256]; batch_job_t jobs[256];
+  for( int t=0; t<nthreads; t++ ) {
+    jobs[t] = (batch_job_t){ n, sig, pub, data, msg_off, msg_sz, out, n*(u64)t/(u64)nthreads, n*(u64)(t+1)/(u64)nthreads };
+    if( nthreads==1 ) batch_worker( &jobs[t] );
+    else pthread_create( &th[t], NULL, batch_worker, &jobs[t] );
+  }
+  if( nthreads > 1 ) for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
+}
+
+/* ---------------------------------------------------------------- */
+/* Test-corpus signing (not on the verify path).  Plain RFC 8032 signing
+   with a textbook extended-coordinates add/double-and-add; only the
+   canonical output bytes matter here, so it uses the same field
+   primitives without any claim of limb-exactness.  Mirrors what
+   fd_ed25519_public_from_private / fd_ed25519_sign produce
+   (fd_ed25519_user.c:220-343); tests cross-check signatures against the
+   reference verifier. */
+
+static void fe_invert( fe * out, fe const * z ) {
+  /* z^(p-2) by square-and-multiply over the fixed exponent */
+  static u8 const e[32] = { 0xeb,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,
+                            0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0xff,0x7f };
+  fe r; fe_set( &r, 1 );
+  for( int i=254; i>=0; i-- ) {
+    fe_sq_avx( &r, &r );
+    if( (e[i>>3] >> (i&7)) & 1 ) fe_mul_avx( &r, &r, z );
+  }
+  *out = r;
+}
+
+static void ge_add_full( ge_p3 * r, ge_p3 const * p, ge_p3 const * q ) {
+  fe a, b, c, d, t, e, f, g, h;
+  fe_sub( &a, &p->Y, &p->X ); fe_sub( &t, &q->Y, &q->X ); fe_mul_avx( &a, &a, &t );
+  fe_add( &b, &p->Y, &p->X ); fe_add( &t, &q->Y, &q->X ); fe_mul_avx( &b, &b, &t );
+  fe_mul_avx( &c, &p->T, &q->T ); fe_mul_avx( &c, &c, &FD_ORACLE_D2 );
+  fe_mul_avx( &d, &p->Z, &q->Z ); fe_add( &d, &d, &d );
+  fe_sub( &e, &b, &a ); fe_sub( &f, &d, &c ); fe_add( &g, &d, &c ); fe_add( &h, &b, &a );
+  fe_mul_avx( &r->X, &e, &f ); fe_mul_avx( &r->Y, &g, &h ); fe_mul_avx( &r->T, &e, &h ); fe_mul_avx( &r->Z, &f, &g );
+}
+
+static void ge_base( ge_p3 * B ) {
+  static u8 const by[32] = { 0x58,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,
+                             0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66,0x66 };
+  ge_frombytes_lane( B, by );
+}
+
+static void ge_scalarmult_base_simple( ge_p3 * r, u8 const * a ) {
+  ge_p3 B, acc; ge_base( &B );
+  fe_set( &acc.X, 0 ); fe_set( &acc.Y, 1 ); fe_set( &acc.Z, 1 ); fe_set( &acc.T, 0 );
+  for( int i=255; i>=0; i-- ) {
+    ge_add_full( &acc, &acc, &acc );
+    if( (a[i>>3] >> (i&7)) & 1 ) ge_add_full( &acc, &acc, &B );
+  }
+  *r = acc;
+}
+
+static void ge_p3_tobytes( u8 * s, ge_p3 const * p ) {
+  fe zi, x, y; fe_invert( &zi, &p->Z );
+  fe_mul_avx( &x, &p->X, &zi ); fe_mul_avx( &y, &p->Y, &zi );
+  fe_tobytes( s, &y );
+  s[31] ^= (u8)(fe_isnegative( &x ) << 7);
+}
+
+/* out = (a*b + c) mod L, 32-byte little endian scalars */
+static void sc_muladd_simple( u8 * out, u8 const * a, u8 const * b, u8 const * c ) {
+  u64 acc[64]; memset( acc, 0, sizeof(acc) );
+  for( int i=0; i<32; i++ ) for( int j=0; j<32; j++ ) acc[i+j] += (u64)a[i]*(u64)b[j];
+  for( int i=0; i<32; i++ ) acc[i] += c[i];
+  u8 wide[64]; u64 carry = 0;
+  for( int i=0; i<64; i++ ) { u64 v = acc[i] + carry; wide[i] = (u8)v; carry = v >> 8; }
+  oracle_sc_reduce( wide, out );
+}
+
+EXPORT void oracle_public_from_private( u8 * pub, u8 const * priv ) {
+  u8 h[64]; sha512_3( h, priv, 32, NULL, 0, NULL, 0 );
+  h[0] &= 248; h[31] &= 63; h[31] |= 64;
+  ge_p3 A; ge_scalarmult_base_simple( &A, h );
+  ge_p3_tobytes( pub, &A );
+}
+
+EXPORT void oracle_sign( u8 * sig, u8 const * msg, u64 sz, u8 const * pub, u8 const * priv ) {
+  u8 az[64]; sha512_3( az, priv, 32, NULL, 0, NULL, 0 );
+  az[0] &= 248; az[31] &= 63; az[31] |= 64;
+  u8 nonce[64]; sha512_3( nonce, az+32, 32, msg, sz, NULL, 0 );
+  u8 r[32]; oracle_sc_reduce( nonce, r );
+  ge_p3 R; ge_scalarmult_base_simple( &R, r );
+  ge_p3_tobytes( sig, &R );
+  u8 hram[64]; sha512_3( hram, sig, 32, pub, 32, msg, sz );
+  u8 k[32]; oracle_sc_reduce( hram, k );
+  sc_muladd_simple( sig+32, k, az, r );
+}
+
+/* Batch signer for corpus generation: key i from seed[i*32], message
+   at data+msg_off[i] (msg_sz[i] bytes). */
+typedef struct { u64 lo, hi; u8 const * seed; u8 const * data; u64 const * msg_off; u32 const * msg_sz; u8 * pub; u8 * sig; } sign_job_t;
+static void * sign_worker( void * arg ) {
+  sign_job_t * j = (sign_job_t *)arg;
+  for( u64 i=j->lo; i<j->hi; i++ ) {
+    oracle_public_from_private( j->pub + 32*i, j->seed + 32*i );
+    oracle_sign( j->sig + 64*i, j->data + j->msg_off[i], j->msg_sz[i], j->pub + 32*i, j->seed + 32*i );
+  }
+  return NULL;
+}
+EXPORT void oracle_sign_batch( u64 n, u8 const * seed, u8 const * data, u64 const * msg_off, u32 const * msg_sz,
+                               u8 * pub, u8 * sig, int nthreads ) {
+  if( nthreads < 1 ) nthreads = 1;
+  if( nthreads > 256 ) nthreads = 256;
+  pthread_t th[256]; sign_job_t jobs[256];
+  for( int t=0; t<nthreads; t++ ) {
+    jobs[t] = (sign_job_t){ n*(u64)t/(u64)nthreads, n*(u64)(t+1)/(u64)nthreads, seed, data, msg_off, msg_sz, pub, sig };
+    if( nthreads==1 ) sign_worker( &jobs[t] ); else pthread_create( &th[t], NULL, sign_worker, &jobs[t] );
+  }
+  if( nthreads > 1 ) for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
+}
