@@ -1,0 +1,200 @@
+"""firedancer_amd -- MI355X-native Ed25519 signature verification engine.
+
+Drop-in for tinydancer-io/firedancer's sigverify hot path
+(``fd_ed25519_verify``, src/ballet/ed25519/fd_ed25519.h:96-101).  The
+product is the C-ABI shared library ``libfd_ed25519_gpu.so`` (HIP kernels
+for gfx950 + host runtime, declared in ``include/fd_ed25519_gpu.h``).
+This module is a thin ctypes mirror of that ABI for tests, benchmarks
+and Python callers; it never verifies anything itself and raises if the
+library or a gfx950 device is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfd_ed25519_gpu.so")
+
+SUCCESS = 0
+ERR_SIG = -1
+ERR_PUBKEY = -2
+ERR_MSG = -3
+ERR_ARG = -16
+ERR_GPU = -17
+
+DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"), ("msg_sz", "<u4")])
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load the product library (fails loudly when it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C firedancer_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ul, ip = ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int
+        L.fd_ed25519_verify.argtypes = [vp, ul, vp, vp, vp]
+        L.fd_ed25519_verify.restype = ip
+        L.fd_ed25519_strerror.argtypes = [ip]
+        L.fd_ed25519_strerror.restype = ctypes.c_char_p
+        L.fd_ed25519_verify_batch.argtypes = [ul, vp, vp, vp, vp, vp]
+        L.fd_ed25519_verify_batch.restype = ip
+        L.fd_ed25519_verify_batch_single_msg.argtypes = [vp, ul, vp, vp, ul, vp]
+        L.fd_ed25519_verify_batch_single_msg.restype = ip
+        L.fd_ed25519_gpu_new.argtypes = [ip, ul, ul]
+        L.fd_ed25519_gpu_new.restype = vp
+        L.fd_ed25519_gpu_delete.argtypes = [vp]
+        L.fd_ed25519_gpu_delete.restype = None
+        L.fd_ed25519_gpu_verify_packed.argtypes = [vp, ul, vp, ul, vp, vp]
+        L.fd_ed25519_gpu_verify_packed.restype = ip
+        L.fd_ed25519_gpu_verify_dev.argtypes = [vp, ul, vp, vp, vp, vp]
+        L.fd_ed25519_gpu_verify_dev.restype = ip
+        L.fd_ed25519_gpu_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fd_ed25519_gpu_submit.restype = ip
+        L.fd_ed25519_gpu_poll.argtypes = [vp, ul, vp, ip]
+        L.fd_ed25519_gpu_poll.restype = ip
+        L.fd_ed25519_gpu_depth.argtypes = [vp]
+        L.fd_ed25519_gpu_depth.restype = ip
+        L.fd_ed25519_gpu_device.argtypes = [vp]
+        L.fd_ed25519_gpu_device.restype = ip
+        L.fd_ed25519_gpu_last_error.argtypes = []
+        L.fd_ed25519_gpu_last_error.restype = ctypes.c_char_p
+        L.fd_ed25519_gpu_device_cnt.argtypes = []
+        L.fd_ed25519_gpu_device_cnt.restype = ip
+        L.fd_ed25519_public_from_private.argtypes = [vp, vp, vp]
+        L.fd_ed25519_public_from_private.restype = vp
+        L.fd_ed25519_sign.argtypes = [vp, vp, ul, vp, vp, vp]
+        L.fd_ed25519_sign.restype = vp
+        L.fd_ed25519_sign_batch.argtypes = [ul, vp, vp, vp, vp, vp, vp, ip]
+        L.fd_ed25519_sign_batch.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def strerror(err: int) -> str:
+    return lib().fd_ed25519_strerror(err).decode()
+
+
+def last_error() -> str:
+    return (lib().fd_ed25519_gpu_last_error() or b"").decode()
+
+
+class Engine:
+    """One verification engine bound to one gfx950 device (fd_ed25519_gpu_t)."""
+
+    def __init__(self, device: int = 0, max_sigs: int = 1 << 16, max_blob: int = 1 << 26):
+        L = lib()
+        self._h = L.fd_ed25519_gpu_new(device, max_sigs, max_blob)
+        if not self._h:
+            raise EngineError(f"fd_ed25519_gpu_new(device={device}) failed: {last_error()}")
+        self.device = device
+        self.max_sigs = max_sigs
+        self.max_blob = max_blob
+
+    def close(self):
+        if self._h:
+            lib().fd_ed25519_gpu_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify_packed(self, blob: np.ndarray, desc: np.ndarray) -> np.ndarray:
+        """Host batch in, host codes out (synchronous)."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        out = np.empty(len(desc), dtype=np.int32)
+        err = lib().fd_ed25519_gpu_verify_packed(self._h, len(desc), _p(blob), blob.nbytes, _p(desc), _p(out))
+        if err:
+            raise EngineError(f"verify_packed: {strerror(err)}: {last_error()}")
+        return out
+
+    def verify_dev(self, n: int, d_blob: int, d_desc: int, d_out: int, stream: int = 0) -> None:
+        """Device-resident batch (raw device pointers, e.g. torch tensor .data_ptr())."""
+        err = lib().fd_ed25519_gpu_verify_dev(self._h, n, d_blob, d_desc, d_out, stream or None)
+        if err:
+            raise EngineError(f"verify_dev: {strerror(err)}: {last_error()}")
+
+    def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
+        t = ctypes.c_ulong(0)
+        err = lib().fd_ed25519_gpu_submit(self._h, len(desc), _p(blob), blob.nbytes, _p(desc), ctypes.byref(t))
+        if err:
+            raise EngineError(f"submit: {strerror(err)}: {last_error()}")
+        return t.value
+
+    def poll(self, ticket: int, out: np.ndarray, block: bool = True) -> bool:
+        r = lib().fd_ed25519_gpu_poll(self._h, ticket, _p(out), 1 if block else 0)
+        if r < 0:
+            raise EngineError(f"poll: {strerror(r)}: {last_error()}")
+        return r == 1
+
+    @property
+    def depth(self) -> int:
+        return lib().fd_ed25519_gpu_depth(self._h)
+
+
+def verify(msg: bytes, sig: bytes, pub: bytes) -> int:
+    """fd_ed25519_verify on the process-default engine."""
+    m = ctypes.create_string_buffer(bytes(msg), max(1, len(msg)))
+    s = ctypes.create_string_buffer(bytes(sig), 64)
+    p = ctypes.create_string_buffer(bytes(pub), 32)
+    return lib().fd_ed25519_verify(m, len(msg), s, p, None)
+
+
+def verify_batch(msgs, sigs, pubs) -> tuple[int, np.ndarray]:
+    """fd_ed25519_verify_batch over Python byte strings."""
+    n = len(msgs)
+    bufs = [ctypes.create_string_buffer(bytes(m), max(1, len(m))) for m in msgs]
+    sb = [ctypes.create_string_buffer(bytes(s), 64) for s in sigs]
+    pb = [ctypes.create_string_buffer(bytes(p), 32) for p in pubs]
+    MP = ctypes.c_void_p * n
+    mp = MP(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+    sp = MP(*[ctypes.cast(b, ctypes.c_void_p) for b in sb])
+    pp = MP(*[ctypes.cast(b, ctypes.c_void_p) for b in pb])
+    sz = (ctypes.c_ulong * n)(*[len(m) for m in msgs])
+    out = np.zeros(n, dtype=np.int32)
+    r = lib().fd_ed25519_verify_batch(n, mp, sz, sp, pp, _p(out))
+    return r, out
+
+
+def verify_batch_single_msg(msg: bytes, sigs: np.ndarray, pubs: np.ndarray) -> tuple[int, np.ndarray]:
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(-1, 64)
+    pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1, 32)
+    n = len(sigs)
+    m = ctypes.create_string_buffer(bytes(msg), max(1, len(msg)))
+    out = np.zeros(n, dtype=np.int32)
+    r = lib().fd_ed25519_verify_batch_single_msg(m, len(msg), _p(sigs), _p(pubs), n, _p(out))
+    return r, out
+
+
+def device_count() -> int:
+    return lib().fd_ed25519_gpu_device_cnt()
+
+
+def sign_batch(seeds: np.ndarray, blob: np.ndarray, msg_off: np.ndarray, msg_sz: np.ndarray, nthreads: int = 8):
+    """Host signer (test-data generation only): returns (pub[n,32], sig[n,64])."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+    n = len(seeds)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+    msg_sz = np.ascontiguousarray(msg_sz, dtype=np.uint32)
+    pub = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    lib().fd_ed25519_sign_batch(n, _p(seeds), _p(blob), _p(msg_off), _p(msg_sz), _p(pub), _p(sig), nthreads)
+    return pub, sig

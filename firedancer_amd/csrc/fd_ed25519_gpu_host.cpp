@@ -1,0 +1,372 @@
+/* fd_ed25519_gpu_host.cpp -- host runtime of the MI355X Ed25519 engine
+   (the util/gpu shim of SURVEY.md section 7, step 2).
+
+   One engine per device.  The engine owns:
+     - device buffers for one batch of capacity (max_sigs, max_blob) per
+       ring slot: blob, descriptors, result codes and the HBM working set;
+     - FD_GPU_DEPTH pinned host slots (blob, desc, out) and one HIP stream
+       per slot, so batch b+1's H2D copy overlaps batch b's kernels and
+       batch b-1's D2H copy (double/triple buffering);
+   All allocation happens in fd_ed25519_gpu_new (the verify tile calls it
+   from init(), before the sandbox closes the syscalls HIP needs,
+   src/app/frank/fd_frank_verify.c:7-20).
+
+   Nothing here verifies on the CPU: every code comes from the device. */
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+#include <atomic>
+#include "fd_ed25519_gpu_private.h"
+
+#define FD_GPU_DEPTH 3
+#define FD_BLOB_PAD  64UL
+
+struct fd_ed25519_gpu_slot {
+  /* pinned host staging */
+  uint8_t *               h_blob;
+  fd_ed25519_gpu_desc_t * h_desc;
+  int32_t *               h_out;
+  /* device */
+  uint8_t *               d_blob;
+  fd_ed25519_gpu_desc_t * d_desc;
+  int32_t *               d_out;
+  fd_ed25519_gpu_work_t   work;
+  void *                  d_work_base;
+  hipStream_t             stream;
+  hipEvent_t              done;
+  unsigned long           n;
+  unsigned long           ticket;   /* 0 = free */
+};
+
+struct fd_ed25519_gpu {
+  int           device;
+  unsigned long max_sigs;
+  unsigned long max_blob;
+  unsigned long next_ticket;
+  fd_ed25519_gpu_slot slot[FD_GPU_DEPTH];
+  std::mutex    lock;
+};
+
+static thread_local char fd_gpu_err[256];
+
+static int fd_gpu_fail( char const * what, hipError_t e ) {
+  snprintf( fd_gpu_err, sizeof(fd_gpu_err), "%s: %s", what, hipGetErrorString( e ) );
+  return FD_ED25519_ERR_GPU;
+}
+
+#define HIPCHK(call) do { hipError_t e_ = (call); if( e_ != hipSuccess ) { fd_gpu_fail( #call, e_ ); goto fail; } } while(0)
+
+extern "C" char const * fd_ed25519_gpu_last_error( void ) { return fd_gpu_err; }
+
+extern "C" int fd_ed25519_gpu_device_cnt( void ) {
+  int cnt = 0;
+  if( hipGetDeviceCount( &cnt ) != hipSuccess ) return 0;
+  int ok = 0;
+  for( int d=0; d<cnt; d++ ) {
+    hipDeviceProp_t p;
+    if( hipGetDeviceProperties( &p, d ) != hipSuccess ) continue;
+    if( !strncmp( p.gcnArchName, "gfx950", 6 ) ) ok++;
+  }
+  return ok;
+}
+
+static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long N ) {
+  uint8_t * p = (uint8_t *)base;
+  w->tab      = (int32_t *)p; p += 1280UL * N;
+  w->pts      = (int32_t *)p; p +=  320UL * N;
+  w->status   = (int32_t *)p; p +=    4UL * N;
+  w->pstat    = (int32_t *)p; p +=    8UL * N;
+  w->slides_k = (int8_t  *)p; p +=  256UL * N;
+  w->slides_s = (int8_t  *)p; p +=  256UL * N;
+}
+
+extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob ) {
+  if( !max_sigs || max_sigs > (1UL<<28) || max_blob > (1UL<<32) - FD_BLOB_PAD ) {
+    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_new: bad capacity" );
+    return NULL;
+  }
+  int cnt = 0;
+  if( hipGetDeviceCount( &cnt ) != hipSuccess || device < 0 || device >= cnt ) {
+    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_new: no HIP device %d (count %d)", device, cnt );
+    return NULL;
+  }
+  hipDeviceProp_t prop;
+  if( hipGetDeviceProperties( &prop, device ) != hipSuccess || strncmp( prop.gcnArchName, "gfx950", 6 ) ) {
+    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_new: device %d is not gfx950", device );
+    return NULL;
+  }
+  fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
+  g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1;
+  unsigned long blob_cap = max_blob + FD_BLOB_PAD;
+  HIPCHK( hipSetDevice( device ) );
+  HIPCHK( fd_ed25519_gpu_upload_tables() );
+  for( int s=0; s<FD_GPU_DEPTH; s++ ) {
+    fd_ed25519_gpu_slot * sl = &g->slot[s];
+    HIPCHK( hipHostMalloc( (void **)&sl->h_blob, blob_cap, hipHostMallocDefault ) );
+    HIPCHK( hipHostMalloc( (void **)&sl->h_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t), hipHostMallocDefault ) );
+    HIPCHK( hipHostMalloc( (void **)&sl->h_out,  max_sigs * sizeof(int32_t), hipHostMallocDefault ) );
+    HIPCHK( hipMalloc( (void **)&sl->d_blob, blob_cap ) );
+    HIPCHK( hipMemset( sl->d_blob, 0, blob_cap ) );
+    HIPCHK( hipMalloc( (void **)&sl->d_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t) ) );
+    HIPCHK( hipMalloc( (void **)&sl->d_out,  max_sigs * sizeof(int32_t) ) );
+    HIPCHK( hipMalloc( &sl->d_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
+    fd_work_carve( &sl->work, sl->d_work_base, max_sigs );
+    HIPCHK( hipStreamCreateWithFlags( &sl->stream, hipStreamNonBlocking ) );
+    HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
+    sl->ticket = 0;
+  }
+  return g;
+fail:
+  fd_ed25519_gpu_delete( g );
+  return NULL;
+}
+
+extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
+  if( !g ) return;
+  hipSetDevice( g->device );
+  for( int s=0; s<FD_GPU_DEPTH; s++ ) {
+    fd_ed25519_gpu_slot * sl = &g->slot[s];
+    if( sl->stream ) hipStreamSynchronize( sl->stream );
+    if( sl->h_blob ) hipHostFree( sl->h_blob );
+    if( sl->h_desc ) hipHostFree( sl->h_desc );
+    if( sl->h_out  ) hipHostFree( sl->h_out );
+    if( sl->d_blob ) hipFree( sl->d_blob );
+    if( sl->d_desc ) hipFree( sl->d_desc );
+    if( sl->d_out  ) hipFree( sl->d_out );
+    if( sl->d_work_base ) hipFree( sl->d_work_base );
+    if( sl->stream ) hipStreamDestroy( sl->stream );
+    if( sl->done   ) hipEventDestroy( sl->done );
+  }
+  delete g;
+}
+
+extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { (void)g; return FD_GPU_DEPTH; }
+extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? g->device : -1; }
+
+/* Bounds check one descriptor against the blob (the reference does no
+   argument checking, fd_ed25519.h:89; malformed txns are dropped
+   upstream by fd_txn_parse -- the batch API reports them itself). */
+static inline int fd_desc_ok( fd_ed25519_gpu_desc_t const * d, unsigned long blob_sz ) {
+  return (unsigned long)d->sig_off + 64UL <= blob_sz
+      && (unsigned long)d->pub_off + 32UL <= blob_sz
+      && (unsigned long)d->msg_off + (unsigned long)d->msg_sz <= blob_sz;
+}
+
+extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob,
+                                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream ) {
+  if( !g || n > g->max_sigs ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st );
+  if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
+  return 0;
+}
+
+/* Stage a batch into a slot's pinned buffers and enqueue copy-in,
+   kernels, copy-out on the slot's stream. */
+static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
+                            unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
+  if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
+  memset( sl->h_blob + blob_sz, 0, FD_BLOB_PAD );
+  /* out-of-bounds descriptors are replaced by a harmless in-bounds one
+     and reported as FD_ED25519_ERR_ARG after the run */
+  int any_bad = 0;
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_ed25519_gpu_desc_t d = desc[i];
+    if( !fd_desc_ok( &d, blob_sz ) ) { any_bad = 1; d.sig_off = d.pub_off = d.msg_off = 0; d.msg_sz = 0; }
+    sl->h_desc[i] = d;
+  }
+  (void)any_bad;
+  hipError_t e;
+  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, blob_sz + FD_BLOB_PAD, hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "H2D blob", e );
+  if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "H2D desc", e );
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "launch", e );
+  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "D2H out", e );
+  if( (e = hipEventRecord( sl->done, sl->stream )) != hipSuccess ) return fd_gpu_fail( "event", e );
+  sl->n = n;
+  return 0;
+}
+
+static void fd_slot_collect( fd_ed25519_gpu_slot * sl, unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, int * out ) {
+  for( unsigned long i=0; i<sl->n; i++ ) out[i] = sl->h_out[i];
+  if( desc ) for( unsigned long i=0; i<sl->n; i++ ) if( !fd_desc_ok( &desc[i], blob_sz ) ) out[i] = FD_ED25519_ERR_ARG;
+}
+
+extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                             fd_ed25519_gpu_desc_t const * desc, int * out ) {
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!desc || !out)) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  /* use a free slot; synchronous callers serialise on the lock */
+  fd_ed25519_gpu_slot * sl = NULL;
+  for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( !g->slot[s].ticket ) sl = &g->slot[s];
+  if( !sl ) { sl = &g->slot[0]; hipEventSynchronize( sl->done ); }
+  int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
+  if( err ) return err;
+  if( (e = hipEventSynchronize( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+  fd_slot_collect( sl, blob_sz, desc, out );
+  return 0;
+}
+
+extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_ed25519_gpu_slot * sl = NULL;
+  for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( !g->slot[s].ticket ) sl = &g->slot[s];
+  if( !sl ) return FD_ED25519_ERR_ARG;   /* ring full: poll first */
+  int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
+  if( err ) return err;
+  /* keep what collect needs for the bounds report */
+  sl->ticket = g->next_ticket++;
+  *ticket = sl->ticket;
+  return 0;
+}
+
+extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
+  if( !g || !ticket ) return FD_ED25519_ERR_ARG;
+  fd_ed25519_gpu_slot * sl = NULL;
+  {
+    std::lock_guard<std::mutex> guard( g->lock );
+    for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
+  }
+  if( !sl ) return FD_ED25519_ERR_ARG;
+  hipError_t e = block ? hipEventSynchronize( sl->done ) : hipEventQuery( sl->done );
+  if( e == hipErrorNotReady ) return 0;
+  if( e != hipSuccess ) return fd_gpu_fail( "poll", e );
+  std::lock_guard<std::mutex> guard( g->lock );
+  if( out ) fd_slot_collect( sl, ~0UL, NULL, out );
+  sl->ticket = 0;
+  return 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* Process-default engine and the reference-shaped APIs. */
+
+static std::mutex          fd_default_lock;
+static fd_ed25519_gpu_t *  fd_default_gpu = NULL;
+static unsigned long       fd_default_sigs = 1UL << 16;
+static unsigned long       fd_default_blob = 1UL << 26;
+
+static fd_ed25519_gpu_t * fd_default_engine( void ) {
+  std::lock_guard<std::mutex> guard( fd_default_lock );
+  if( !fd_default_gpu ) {
+    char const * dev = getenv( "FD_ED25519_GPU_DEVICE" );
+    fd_default_gpu = fd_ed25519_gpu_new( dev ? atoi( dev ) : 0, fd_default_sigs, fd_default_blob );
+  }
+  return fd_default_gpu;
+}
+
+/* Pack pointer-array inputs into a pinned slot blob in chunks of the
+   engine capacity and run them. */
+static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
+                             uint8_t const * shared_msg, unsigned long shared_sz,
+                             uint8_t const * const * sigp, uint8_t const (*siga)[64],
+                             uint8_t const * const * pubp, uint8_t const (*puba)[32], int * out ) {
+  fd_ed25519_gpu_t * g = fd_default_engine();
+  if( !g ) return FD_ED25519_ERR_GPU;
+  std::lock_guard<std::mutex> guard( g->lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_ed25519_gpu_slot * sl = &g->slot[0];
+  hipEventSynchronize( sl->done );
+  unsigned long i = 0;
+  while( i < n ) {
+    /* fill one chunk */
+    unsigned long used = 0, cnt = 0;
+    unsigned long shared_off = 0;
+    if( shared_msg ) {
+      if( shared_sz + 96UL > g->max_blob ) return FD_ED25519_ERR_ARG;
+      memcpy( sl->h_blob, shared_msg, shared_sz ); used = shared_sz;
+    }
+    while( i + cnt < n && cnt < g->max_sigs ) {
+      unsigned long k = i + cnt;
+      unsigned long msz = shared_msg ? 0UL : msg_sz[k];
+      if( msz > 0x7fffffffUL ) return FD_ED25519_ERR_ARG;
+      if( used + 96UL + msz > g->max_blob ) break;
+      fd_ed25519_gpu_desc_t * d = &sl->h_desc[cnt];
+      d->sig_off = (uint32_t)used; memcpy( sl->h_blob + used, sigp ? sigp[k] : siga[k], 64 ); used += 64;
+      d->pub_off = (uint32_t)used; memcpy( sl->h_blob + used, pubp ? pubp[k] : puba[k], 32 ); used += 32;
+      if( shared_msg ) { d->msg_off = (uint32_t)shared_off; d->msg_sz = (uint32_t)shared_sz; }
+      else {
+        d->msg_off = (uint32_t)used; d->msg_sz = (uint32_t)msz;
+        if( msz ) memcpy( sl->h_blob + used, msg[k], msz );
+        used += msz;
+      }
+      cnt++;
+    }
+    if( !cnt ) return FD_ED25519_ERR_ARG;   /* single message larger than the engine's blob */
+    int err = fd_slot_enqueue( g, sl, cnt, sl->h_blob, used, sl->h_desc );
+    if( err ) return err;
+    if( (e = hipEventSynchronize( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+    for( unsigned long k=0; k<cnt; k++ ) out[i+k] = sl->h_out[k];
+    i += cnt;
+  }
+  return 0;
+}
+
+static int fd_first_err( unsigned long n, int const * out ) {
+  for( unsigned long i=0; i<n; i++ ) if( out[i] ) return out[i];
+  return 0;
+}
+
+extern "C" int fd_ed25519_verify_batch( unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
+                                        uint8_t const * const * sig, uint8_t const * const * pub, int * out_err ) {
+  if( !n ) return 0;
+  if( !msg || !msg_sz || !sig || !pub || !out_err ) return FD_ED25519_ERR_ARG;
+  for( unsigned long i=0; i<n; i++ ) if( !sig[i] || !pub[i] || (msg_sz[i] && !msg[i]) ) return FD_ED25519_ERR_ARG;
+  int err = fd_run_ptr_batch( n, msg, msg_sz, NULL, 0, sig, NULL, pub, NULL, out_err );
+  if( err ) return err;
+  return fd_first_err( n, out_err );
+}
+
+extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned long msg_sz, uint8_t const (*sig)[64],
+                                                   uint8_t const (*pub)[32], unsigned long n, int * out_err_opt ) {
+  if( !n ) return 0;
+  if( !sig || !pub || (msg_sz && !msg) ) return FD_ED25519_ERR_ARG;
+  int * out = out_err_opt;
+  int * tmp = NULL;
+  if( !out ) { tmp = (int *)malloc( n * sizeof(int) ); if( !tmp ) return FD_ED25519_ERR_GPU; out = tmp; }
+  static uint8_t const empty[1] = { 0 };
+  int err = fd_run_ptr_batch( n, NULL, NULL, msg_sz ? msg : empty, msg_sz, NULL, sig, NULL, pub, out );
+  int r = err ? err : fd_first_err( n, out );
+  free( tmp );
+  return r;
+}
+
+extern "C" int fd_ed25519_verify( void const * msg, unsigned long sz, void const * sig, void const * public_key, void * sha ) {
+  (void)sha;
+  uint8_t const * m = (uint8_t const *)msg;
+  uint8_t const * s = (uint8_t const *)sig;
+  uint8_t const * p = (uint8_t const *)public_key;
+  int out = 0;
+  int err = fd_ed25519_verify_batch( 1UL, &m, &sz, &s, &p, &out );
+  if( err == FD_ED25519_ERR_GPU || err == FD_ED25519_ERR_ARG ) return err;
+  return out;
+}
+
+extern "C" char const * fd_ed25519_strerror( int err ) {
+  switch( err ) {
+  case FD_ED25519_SUCCESS:    return "success";
+  case FD_ED25519_ERR_SIG:    return "bad signature";
+  case FD_ED25519_ERR_PUBKEY: return "bad public key";
+  case FD_ED25519_ERR_MSG:    return "bad message";
+  case FD_ED25519_ERR_ARG:    return "bad argument";
+  case FD_ED25519_ERR_GPU:    return "gpu failure";
+  default: break;
+  }
+  return "unknown";
+}

@@ -1,0 +1,415 @@
+/* fd_ed25519_gpu_kernels.hip -- Ed25519 batch verification on gfx950.
+
+   Reference path replaced: fd_ed25519_verify
+   (src/ballet/ed25519/fd_ed25519_user.c:346-433, AVX2 build).  Results are
+   bit-exact with it, including its quirks.
+
+   A batch is (blob, desc[n]) resident in HBM: desc[i] gives byte offsets
+   of signature i's R||S, public key and message inside the blob.  Three
+   kernels, each one lane per work item, all state SoA ([field][item]) so
+   every global access of a wave is coalesced:
+
+     fd_k_prep      one lane per signature: S-range check (incl. the
+                    early-success quirk Q1), k = SHA-512(R||A||M) mod L,
+                    signed sliding-window recodings of k and S.
+     fd_k_decomp    one lane per POINT (2 per signature): lax
+                    decompression (Q3) and the [8]P small-order test,
+                    the uniform ~265-squaring part of the path.
+     fd_k_dsm       one lane per signature: [k](-A) + [S]B with the
+                    reference's 4-lane AVX operation sequence reproduced
+                    limb-for-limb, then the non-canonical limb compare
+                    (Q2) and the error-code precedence (Q4). */
+
+#include "fd_ed25519_gpu_fe.h"
+#include "fd_ed25519_gpu_sha512.h"
+#include "fd_ed25519_gpu_private.h"
+
+typedef fd_gpu_fe_t  fe;
+typedef fd_gpu_fe4_t fe4;
+#include "fd_ed25519_tables.h"
+
+/* prep status codes (internal) */
+#define FD_ST_PENDING  1
+/* decomp status codes (internal) */
+#define FD_PT_OK       0
+#define FD_PT_BAD      1   /* not on curve           -> ERR_PUBKEY */
+#define FD_PT_SMALL    2   /* small order            -> A: ERR_PUBKEY, R: ERR_SIG */
+
+__constant__ static fe4 fd_gpu_bi_precomp[8];
+
+/* ------------------------------------------------------------------ */
+/* 4-lane vector helpers: the AVX path's wl_t x 10 state, one field
+   element per lane (fd_ed25519_fe_avx.h:32-69). */
+
+FD_DEV void v_mul( fe4 & h, fe4 const & f, fe4 const & g ) {
+  fe4 t;
+#pragma unroll
+  for( int l=0; l<4; l++ ) fd_fe_mul( t.l[l], f.l[l], g.l[l] );
+  h = t;
+}
+FD_DEV void v_mul3( fe4 & h, fe4 const & f, fe4 const & g ) { /* lane 3 unused by consumer */
+  fe4 t;
+#pragma unroll
+  for( int l=0; l<3; l++ ) fd_fe_mul( t.l[l], f.l[l], g.l[l] );
+  t.l[3] = f.l[3];
+  h = t;
+}
+FD_DEV void v_dbl_mix( fe4 & h ) {   /* [a-b-c, b+c, b-c, d-b+c] */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    uint32_t a=h.l[0].v[k], b=h.l[1].v[k], c=h.l[2].v[k], d=h.l[3].v[k];
+    h.l[0].v[k]=(int32_t)(a-b-c); h.l[1].v[k]=(int32_t)(b+c); h.l[2].v[k]=(int32_t)(b-c); h.l[3].v[k]=(int32_t)(d-b+c);
+  }
+}
+FD_DEV void v_sub_mix( fe4 & h ) {   /* [c-b, c+b, 2a-d, 2a+d] */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    uint32_t a=h.l[0].v[k], b=h.l[1].v[k], c=h.l[2].v[k], d=h.l[3].v[k];
+    h.l[0].v[k]=(int32_t)(c-b); h.l[1].v[k]=(int32_t)(c+b); h.l[2].v[k]=(int32_t)(2u*a-d); h.l[3].v[k]=(int32_t)(2u*a+d);
+  }
+}
+FD_DEV void v_subadd_12( fe4 & h ) { /* [a, b-c, b+c, d] */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    uint32_t b=h.l[1].v[k], c=h.l[2].v[k];
+    h.l[1].v[k]=(int32_t)(b-c); h.l[2].v[k]=(int32_t)(b+c);
+  }
+}
+
+/* p2 doubling into p1p1, lanes [X,Y,Z] -> (fd_ed25519_ge.c inline form
+   avx/fd_ed25519_ge.c:493-498): vt = DBL_MIX(SQN([X+Y,Y,X,Z]; 1,1,1,2)) */
+FD_DEV void v_p2_dbl( fe4 & vt, fe const & X, fe const & Y, fe const & Z ) {
+  fe xy; fd_fe_add( xy, X, Y );
+  fd_fe_sqn( vt.l[0], xy, 1 );
+  fd_fe_sqn( vt.l[1], Y,  1 );
+  fd_fe_sqn( vt.l[2], X,  1 );
+  fd_fe_sqn( vt.l[3], Z,  2 );
+  v_dbl_mix( vt );
+}
+
+/* ------------------------------------------------------------------ */
+/* Kernel 1: prep. */
+
+FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
+#pragma unroll
+  for( int i=0; i<8; i++ ) w[i] = fd_ld_u32_unaligned( p + 4*i );
+}
+
+/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) streamed out as
+   signed digits, kept as a 256-bit running value V: a digit absorbing
+   bit i+b by subtraction is the reference's carry loop, i.e. V += 2^(i+b). */
+FD_DEV void fd_slide_write( uint64_t (&a)[4], int8_t * out, uint64_t stride ) {
+  /* V: 5 words so carries past bit 255 are kept (and ignored) */
+  uint64_t V[5] = { a[0], a[1], a[2], a[3], 0 };
+  for( int i=0; i<256; i++ ) {
+    int d = (int)((V[i>>6] >> (i&63)) & 1ULL);
+    if( d ) {
+      for( int b=1; b<=6 && i+b<256; b++ ) {
+        int p = i+b;
+        if( !((V[p>>6] >> (p&63)) & 1ULL) ) continue;
+        int up = 1 << b;
+        if( d + up <= 15 ) {
+          d += up; V[p>>6] &= ~(1ULL << (p&63));
+        } else if( d - up >= -15 ) {
+          d -= up;
+          /* add 2^p to V (bit p is set): ripple-carry over words */
+          int wd = p>>6; uint64_t add = 1ULL << (p&63);
+          for( int k=wd; k<5; k++ ) { uint64_t o = V[k]; V[k] = o + add; add = (V[k] < o) ? 1ULL : 0ULL; if( !add ) break; }
+        } else break;
+      }
+    }
+    out[ (uint64_t)i*stride ] = (int8_t)d;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+           int32_t * __restrict__ status, int8_t * __restrict__ slides_k, int8_t * __restrict__ slides_s ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  fd_ed25519_gpu_desc_t d = desc[i];
+  uint8_t const * R = blob + d.sig_off;
+  uint8_t const * S = R + 32;
+  uint8_t const * A = blob + d.pub_off;
+  uint8_t const * M = blob + d.msg_off;
+
+  uint32_t sw[8]; fd_ld32( sw, S );
+  uint32_t s31 = sw[7] >> 24;
+  /* S range check (fd_ed25519_user.c:372-393) */
+  int st = FD_ST_PENDING;
+  if( s31 > 0x10u ) st = FD_ED25519_ERR_SIG;
+  else if( s31 == 0x10u ) {
+    /* s[16..30] nonzero -> early SUCCESS (Q1, fd_ed25519_user.c:379) */
+    if( sw[4] | sw[5] | sw[6] | (sw[7] & 0x00ffffffu) ) st = FD_ED25519_SUCCESS;
+    else {
+      /* compare s[0..15] against l_low (little endian 128-bit): S >= L -> ERR_SIG */
+      uint64_t lo = ((uint64_t)sw[1] << 32) | sw[0], hi = ((uint64_t)sw[3] << 32) | sw[2];
+      uint64_t llo = 0x5812631a5cf5d3edULL, lhi = 0x14def9dea2f79cd6ULL;
+      if( hi > lhi || (hi == lhi && lo >= llo) ) st = FD_ED25519_ERR_SIG;
+    }
+  }
+  status[i] = st;
+  if( st != FD_ST_PENDING ) return;
+
+  uint64_t dig[8];
+  fd_sha512_ram( dig, R, A, M, d.msg_sz );
+  uint64_t k[4];
+  fd_sc_reduce( k, dig );
+  fd_slide_write( k, slides_k + i, n );
+  uint64_t s[4] = { ((uint64_t)sw[1]<<32)|sw[0], ((uint64_t)sw[3]<<32)|sw[2], ((uint64_t)sw[5]<<32)|sw[4], ((uint64_t)sw[7]<<32)|sw[6] };
+  fd_slide_write( s, slides_s + i, n );
+}
+
+/* ------------------------------------------------------------------ */
+/* Kernel 2: decompress + small order.  Item j < n is A_j (public key),
+   item n+j is R_j.  Output X,Y,Z,T SoA [40][2n]. */
+
+/* fe_avx_pow22523 (avx/fd_ed25519_fe_avx.h:246-275) */
+FD_DEV void fd_pow22523( fe & out, fe const & f ) {
+  fe t0, t1, t2;
+  fd_fe_sq( t0, f );
+  fd_fe_sq( t1, t0 ); fd_fe_sq( t1, t1 );
+  fd_fe_mul( t1, f, t1 );
+  fd_fe_mul( t0, t0, t1 );
+  fd_fe_sq( t0, t0 );
+  fd_fe_mul( t0, t1, t0 );
+  fd_fe_sq( t1, t0 ); for( int i=1; i<5; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( t0, t1, t0 );
+  fd_fe_sq( t1, t0 ); for( int i=1; i<10; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( t1, t1, t0 );
+  fd_fe_sq( t2, t1 ); for( int i=1; i<20; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t1, t2, t1 );
+  fd_fe_sq( t1, t1 ); for( int i=1; i<10; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( t0, t1, t0 );
+  fd_fe_sq( t1, t0 ); for( int i=1; i<50; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( t1, t1, t0 );
+  fd_fe_sq( t2, t1 ); for( int i=1; i<100; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t1, t2, t1 );
+  fd_fe_sq( t1, t1 ); for( int i=1; i<50; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( t0, t1, t0 );
+  fd_fe_sq( t0, t0 ); fd_fe_sq( t0, t0 );
+  fd_fe_mul( out, t0, f );
+}
+
+/* one lane of fd_ed25519_ge_p2_dbl (avx/fd_ed25519_ge.c:127-141) + the
+   p1p1 -> p2 / p3 conversions, for the [8]P test (fd_ed25519_ge.c:21-66) */
+FD_DEV void fd_small_dbl( fe (&r)[4], fe const & X, fe const & Y, fe const & Z ) {
+  fe xy, t0;
+  fd_fe_add( xy, X, Y );
+  fd_fe_sqn( r[0], X, 1 );
+  fd_fe_sqn( r[2], Y, 1 );
+  fd_fe_sqn( r[3], Z, 2 );
+  fd_fe_sqn( t0, xy, 1 );
+  fd_fe_add( r[1], r[2], r[0] );
+  fd_fe_sub( r[2], r[2], r[0] );
+  fd_fe_sub( r[0], t0, r[1] );
+  fd_fe_sub( r[3], r[3], r[2] );
+}
+
+FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
+  int eq = 1;
+#pragma unroll
+  for( int i=0; i<10; i++ ) eq &= (a.v[i] == b.v[i]);
+  return eq;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+             int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts ) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t m = 2*n;
+  if( j >= m ) return;
+  uint64_t i = j < n ? j : j - n;
+  if( status[i] != FD_ST_PENDING ) { pstat[j] = FD_PT_OK; return; }
+  fd_ed25519_gpu_desc_t d = desc[i];
+  uint8_t const * s = blob + (j < n ? d.pub_off : d.sig_off);
+  uint32_t w[8]; fd_ld32( w, s );
+
+  fe y, u, v, vw, x, vxx, check;
+  fd_fe_frombytes( y, w );
+  fd_fe_sq( u, y );
+  fd_fe_mul( v, u, FD_GPU_D );
+  u.v[0] -= 1;
+  v.v[0] += 1;
+  fd_fe_sq( vw, v );
+  fd_fe_mul( vw, vw, v );
+  fd_fe_sq( x, vw );
+  fd_fe_mul( x, x, v );
+  fd_fe_mul( x, x, u );
+  fd_pow22523( x, x );
+  fd_fe_mul( x, x, vw );
+  fd_fe_mul( x, x, u );
+  fd_fe_sq( vxx, x );
+  fd_fe_mul( vxx, vxx, v );
+  fd_fe_sub( check, vxx, u );
+  int bad = 0;
+  if( fd_fe_isnonzero( check ) ) {
+    fd_fe_add( check, vxx, u );
+    if( fd_fe_isnonzero( check ) ) bad = 1;
+    else fd_fe_mul_scalar( x, x, FD_GPU_SQRTM1 );
+  }
+  if( bad ) { pstat[j] = FD_PT_BAD; return; }
+  if( fd_fe_isnegative( x ) != (int)(w[7] >> 31) ) fd_fe_neg( x, x );
+  fe T; fd_fe_mul( T, x, y );
+  fe Z; fd_fe_set( Z, 1 );
+
+  /* store the point */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    pts[(uint64_t)( 0+k)*m + j] = x.v[k];
+    pts[(uint64_t)(10+k)*m + j] = y.v[k];
+    pts[(uint64_t)(20+k)*m + j] = Z.v[k];
+    pts[(uint64_t)(30+k)*m + j] = T.v[k];
+  }
+
+  /* small order: [8]P == identity by limb equality */
+  fe X2 = x, Y2 = y, Z2 = Z, r[4];
+  for( int it=0; it<2; it++ ) {
+    fd_small_dbl( r, X2, Y2, Z2 );
+    fd_fe_mul( X2, r[0], r[3] ); fd_fe_mul( Y2, r[1], r[2] ); fd_fe_mul( Z2, r[2], r[3] );
+  }
+  fd_small_dbl( r, X2, Y2, Z2 );
+  fe tX, tY, tZ;
+  fd_fe_mul( tX, r[0], r[3] ); fd_fe_mul( tY, r[1], r[2] ); fd_fe_mul( tZ, r[2], r[3] );
+  /* is_identity (fd_ed25519_ge.c:41-59): mul(X,1)==mul(0,Z), mul(Y,1)==mul(1,Z) */
+  fe one, zero, c0, c1; fd_fe_set( one, 1 ); fd_fe_set( zero, 0 );
+  fd_fe_mul_scalar( c0, tX, one ); fd_fe_mul_scalar( c1, zero, tZ );
+  int ix = fd_limbs_eq( c0, c1 );
+  fd_fe_mul_scalar( c0, tY, one ); fd_fe_mul_scalar( c1, one, tZ );
+  int iy = fd_limbs_eq( c0, c1 );
+  pstat[j] = (ix & iy) ? FD_PT_SMALL : FD_PT_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Kernel 3: double-scalar multiplication + compare.  Ai (the 8 odd
+   multiples of -A in cached form) is kept in a per-signature SoA scratch
+   table [8][4][10][n] in HBM (L2-resident while the launch runs). */
+
+FD_DEV void fd_tab_store( int32_t * tab, uint64_t n, uint64_t i, int e, fe4 const & v ) {
+#pragma unroll
+  for( int l=0; l<4; l++ )
+#pragma unroll
+    for( int k=0; k<10; k++ ) tab[((uint64_t)(e*40 + l*10 + k))*n + i] = v.l[l].v[k];
+}
+FD_DEV void fd_tab_load( fe4 & v, int32_t const * tab, uint64_t n, uint64_t i, int e ) {
+#pragma unroll
+  for( int l=0; l<4; l++ )
+#pragma unroll
+    for( int k=0; k<10; k++ ) v.l[l].v[k] = tab[((uint64_t)(e*40 + l*10 + k))*n + i];
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+          int32_t const * __restrict__ pts, int8_t const * __restrict__ slides_k, int8_t const * __restrict__ slides_s,
+          int32_t * __restrict__ tab, int32_t * __restrict__ out ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  uint64_t m = 2*n;
+  int st = status[i];
+  if( st != FD_ST_PENDING ) { out[i] = st; return; }
+  int pa = pstat[i], pr = pstat[n+i];
+  /* error precedence (fd_ed25519_user.c:401-403) */
+  if( pa == FD_PT_BAD || pr == FD_PT_BAD ) { out[i] = FD_ED25519_ERR_PUBKEY; return; }
+  if( pa == FD_PT_SMALL ) { out[i] = FD_ED25519_ERR_PUBKEY; return; }
+  if( pr == FD_PT_SMALL ) { out[i] = FD_ED25519_ERR_SIG;    return; }
+
+  fe4 vr, vt, vu;
+  /* vr = [Z, Y, X, T] of -A (fd_ed25519_user.c:408-409 negates X, T) */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + i]);
+    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + i];
+    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + i];
+    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + i]);
+  }
+
+  /* Ai = {A,3A,...,15A} cached (avx/fd_ed25519_ge.c:423-481) */
+  fe4 d111;
+#pragma unroll
+  for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
+  d111.l[3] = FD_GPU_D2;
+  v_mul( vu, vr, d111 ); v_subadd_12( vu );
+  fd_tab_store( tab, n, i, 0, vu );
+  /* A2 = dbl(A): vt = perm(vr,2,1,2,0) + [Y,0,0,0] -> [X+Y, Y, X, Z] */
+  v_p2_dbl( vt, vr.l[2], vr.l[1], vr.l[0] );
+  {
+    fe4 a, b;   /* vr = MUL(perm(vt,3,2,3,1), perm(vt,2,1,0,0)) */
+    a.l[0]=vt.l[3]; a.l[1]=vt.l[2]; a.l[2]=vt.l[3]; a.l[3]=vt.l[1];
+    b.l[0]=vt.l[2]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
+    v_mul( vr, a, b );
+  }
+  v_subadd_12( vr );
+  for( int e=0; e<7; e++ ) {
+    v_mul( vt, vr, vu );
+    v_sub_mix( vt );
+    fe4 a, b;   /* vt = MUL(perm(vt,2,3,2,1), perm(vt,3,1,0,0)) */
+    a.l[0]=vt.l[2]; a.l[1]=vt.l[3]; a.l[2]=vt.l[2]; a.l[3]=vt.l[1];
+    b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
+    v_mul( vt, a, b );
+    v_mul( vu, vt, d111 ); v_subadd_12( vu );
+    fd_tab_store( tab, n, i, e+1, vu );
+  }
+
+  /* main loop (avx/fd_ed25519_ge.c:483-523); leading iterations on the
+     identity are exact no-ops (doubling (0:1:1) returns the same limbs),
+     so every lane runs the full 256 bits. */
+  fe X, Y, Z;
+  fd_fe_set( X, 0 ); fd_fe_set( Y, 1 ); fd_fe_set( Z, 1 );
+  for( int b=255; b>=0; b-- ) {
+    v_p2_dbl( vt, X, Y, Z );
+    for( int j=0; j<2; j++ ) {
+      int sl = j ? (int)slides_s[(uint64_t)b*n + i] : (int)slides_k[(uint64_t)b*n + i];
+      if( sl ) {
+        fe4 a, c;   /* p1p1 -> p3: MUL(perm(vt,2,1,0,0), perm(vt,3,2,3,1)) */
+        a.l[0]=vt.l[2]; a.l[1]=vt.l[1]; a.l[2]=vt.l[0]; a.l[3]=vt.l[0];
+        c.l[0]=vt.l[3]; c.l[1]=vt.l[2]; c.l[2]=vt.l[3]; c.l[3]=vt.l[1];
+        v_mul( vt, a, c );
+        int e = (sl < 0 ? -sl : sl) >> 1;
+        if( j ) vu = fd_gpu_bi_precomp[e];
+        else    fd_tab_load( vu, tab, n, i, e );
+        if( sl < 0 ) { fe t = vu.l[1]; vu.l[1] = vu.l[2]; vu.l[2] = t; }
+        v_subadd_12( vt );
+        v_mul( vt, vt, vu );
+        v_sub_mix( vt );
+        if( sl > 0 ) { fe t = vt.l[2]; vt.l[2] = vt.l[3]; vt.l[3] = t; }
+      }
+    }
+    /* p1p1 -> p2: MUL(vt, perm(vt,3,2,3,3)) */
+    fd_fe_mul( X, vt.l[0], vt.l[3] );
+    fd_fe_mul( Y, vt.l[1], vt.l[2] );
+    fd_fe_mul( Z, vt.l[2], vt.l[3] );
+  }
+
+  /* compare r.x*R.Z == R.X and r.y*R.Z == R.Y on limbs 0..7 (Q2) */
+  fe rx, ry;
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    rx.v[k] = pts[(uint64_t)( 0+k)*m + n + i];
+    ry.v[k] = pts[(uint64_t)(10+k)*m + n + i];
+  }
+  fe xz, yz;
+  fd_fe_mul( xz, Z, rx );
+  fd_fe_mul( yz, Z, ry );
+  int eq = 1;
+#pragma unroll
+  for( int k=0; k<8; k++ ) eq &= (xz.v[k] == X.v[k]) & (yz.v[k] == Y.v[k]);
+  out[i] = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+/* ------------------------------------------------------------------ */
+/* Host-side launch (C ABI, used by fd_ed25519_gpu_host.cpp). */
+
+extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
+  return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_precomp), FD_GPU_BI_PRECOMP, sizeof(FD_GPU_BI_PRECOMP) );
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream ) {
+  if( !n ) return hipSuccess;
+  unsigned nb  = (unsigned)((n + 255) / 256);
+  unsigned nb2 = (unsigned)((2*n + 255) / 256);
+  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->slides_k, w->slides_s );
+  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts );
+  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->slides_k, w->slides_s, w->tab, out );
+  return hipGetLastError();
+}

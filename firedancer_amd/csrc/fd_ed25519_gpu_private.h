@@ -1,0 +1,37 @@
+/* fd_ed25519_gpu_private.h -- engine internals shared by host and kernels. */
+#ifndef FD_ED25519_GPU_PRIVATE_H
+#define FD_ED25519_GPU_PRIVATE_H
+
+#include <hip/hip_runtime.h>
+#include "fd_ed25519_gpu.h"
+
+/* Per-batch HBM working set, SoA [field][item] (sizes for capacity N):
+     status   int32 [N]          prep result (S check) or pending
+     slides_k int8  [256][N]     signed window digits of k
+     slides_s int8  [256][N]     signed window digits of S
+     pstat    int32 [2N]         point status, A then R
+     pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
+     tab      int32 [320][N]     per-signature Ai table (8 x 4 lanes x 10) */
+typedef struct fd_ed25519_gpu_work {
+  int32_t * status;
+  int8_t  * slides_k;
+  int8_t  * slides_s;
+  int32_t * pstat;
+  int32_t * pts;
+  int32_t * tab;
+} fd_ed25519_gpu_work_t;
+
+/* bytes of HBM working set per signature of capacity */
+#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 512UL + 8UL + 320UL + 1280UL)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+hipError_t fd_ed25519_gpu_upload_tables( void );
+hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                  fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream );
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,162 @@
+/* fd_ed25519_gpu_sha512.h -- SHA-512 and scalar reduction (device).
+
+   k = SHA-512(R || A || M) mod L, one lane per signature
+   (src/ballet/ed25519/fd_ed25519_user.c:411-414; SHA-512 streaming
+   semantics of src/ballet/sha512/fd_sha512.c:265-399; reduction
+   schedule of fd_ed25519_sc_reduce, fd_ed25519_user.c:3-110). */
+
+#ifndef FD_ED25519_GPU_SHA512_H
+#define FD_ED25519_GPU_SHA512_H
+
+#include "fd_ed25519_gpu_fe.h"
+
+__constant__ static uint64_t const fd_gpu_sha512_k[80] = {
+  0x428a2f98d728ae22ULL,0x7137449123ef65cdULL,0xb5c0fbcfec4d3b2fULL,0xe9b5dba58189dbbcULL,0x3956c25bf348b538ULL,
+  0x59f111f1b605d019ULL,0x923f82a4af194f9bULL,0xab1c5ed5da6d8118ULL,0xd807aa98a3030242ULL,0x12835b0145706fbeULL,
+  0x243185be4ee4b28cULL,0x550c7dc3d5ffb4e2ULL,0x72be5d74f27b896fULL,0x80deb1fe3b1696b1ULL,0x9bdc06a725c71235ULL,
+  0xc19bf174cf692694ULL,0xe49b69c19ef14ad2ULL,0xefbe4786384f25e3ULL,0x0fc19dc68b8cd5b5ULL,0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL,0x4a7484aa6ea6e483ULL,0x5cb0a9dcbd41fbd4ULL,0x76f988da831153b5ULL,0x983e5152ee66dfabULL,
+  0xa831c66d2db43210ULL,0xb00327c898fb213fULL,0xbf597fc7beef0ee4ULL,0xc6e00bf33da88fc2ULL,0xd5a79147930aa725ULL,
+  0x06ca6351e003826fULL,0x142929670a0e6e70ULL,0x27b70a8546d22ffcULL,0x2e1b21385c26c926ULL,0x4d2c6dfc5ac42aedULL,
+  0x53380d139d95b3dfULL,0x650a73548baf63deULL,0x766a0abb3c77b2a8ULL,0x81c2c92e47edaee6ULL,0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL,0xa81a664bbc423001ULL,0xc24b8b70d0f89791ULL,0xc76c51a30654be30ULL,0xd192e819d6ef5218ULL,
+  0xd69906245565a910ULL,0xf40e35855771202aULL,0x106aa07032bbd1b8ULL,0x19a4c116b8d2d0c8ULL,0x1e376c085141ab53ULL,
+  0x2748774cdf8eeb99ULL,0x34b0bcb5e19b48a8ULL,0x391c0cb3c5c95a63ULL,0x4ed8aa4ae3418acbULL,0x5b9cca4f7763e373ULL,
+  0x682e6ff3d6b2b8a3ULL,0x748f82ee5defb2fcULL,0x78a5636f43172f60ULL,0x84c87814a1f0ab72ULL,0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL,0xa4506cebde82bde9ULL,0xbef9a3f7b2c67915ULL,0xc67178f2e372532bULL,0xca273eceea26619cULL,
+  0xd186b8c721c0c207ULL,0xeada7dd6cde0eb1eULL,0xf57d4f7fee6ed178ULL,0x06f067aa72176fbaULL,0x0a637dc5a2c898a6ULL,
+  0x113f9804bef90daeULL,0x1b710b35131c471bULL,0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,
+  0x431d67c49c100d4cULL,0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL
+};
+
+FD_DEV uint64_t fd_rotr64( uint64_t x, int n ) { return (x >> n) | (x << (64-n)); }
+FD_DEV uint64_t fd_bswap64( uint64_t x ) { return __builtin_bswap64( x ); }
+
+/* 4 bytes at an arbitrary byte address, little endian; reads the
+   enclosing aligned words (the batch blob is padded by >= 16 bytes). */
+FD_DEV uint32_t fd_ld_u32_unaligned( uint8_t const * p ) {
+  uintptr_t a = (uintptr_t)p;
+  uint32_t const * w = (uint32_t const *)(a & ~(uintptr_t)3);
+  uint32_t lo = w[0], hi = w[1];
+  uint32_t sh = (uint32_t)(a & 3u) * 8u;
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+}
+
+FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
+  uintptr_t a = (uintptr_t)p;
+  uint32_t const * w = (uint32_t const *)(a & ~(uintptr_t)3);
+  uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  uint32_t sh = (uint32_t)(a & 3u) * 8u;
+  uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
+  uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
+  uint64_t a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
+#pragma unroll
+  for( int t=0; t<80; t++ ) {
+    if( t>=16 ) {
+      uint64_t w15 = w[(t-15)&15], w2 = w[(t-2)&15];
+      uint64_t s0 = fd_rotr64(w15,1) ^ fd_rotr64(w15,8) ^ (w15>>7);
+      uint64_t s1 = fd_rotr64(w2,19) ^ fd_rotr64(w2,61) ^ (w2>>6);
+      w[t&15] = w[t&15] + s0 + w[(t-7)&15] + s1;
+    }
+    uint64_t S1 = fd_rotr64(e,14) ^ fd_rotr64(e,18) ^ fd_rotr64(e,41);
+    uint64_t ch = (e&f) ^ (~e&g);
+    uint64_t t1 = h + S1 + ch + fd_gpu_sha512_k[t] + w[t&15];
+    uint64_t S0 = fd_rotr64(a,28) ^ fd_rotr64(a,34) ^ fd_rotr64(a,39);
+    uint64_t mj = (a&b) ^ (a&c) ^ (b&c);
+    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;
+  }
+  st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
+}
+
+/* SHA-512 of R(32) || A(32) || M(sz).  Words never straddle the R/A/M
+   boundaries (32 and 64 are multiples of 8).  Returns the digest as 8
+   little-endian-loaded 64-bit words (digest bytes 8i..8i+7 in word i,
+   byte 8i in the low byte). */
+FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
+  uint64_t st[8] = { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL };
+  uint64_t L = 64ULL + sz;                           /* bytes hashed */
+  uint32_t nblk = (uint32_t)((L + 17ULL + 127ULL) >> 7);
+  for( uint32_t b=0; b<nblk; b++ ) {
+    uint64_t w[16];
+#pragma unroll
+    for( int i=0; i<16; i++ ) {
+      uint64_t pos = ((uint64_t)b << 7) + 8u*(uint64_t)i;
+      uint64_t v;                                   /* bytes as loaded little endian */
+      if( pos < 32 )       v = fd_ld_u64_unaligned( R + pos );
+      else if( pos < 64 )  v = fd_ld_u64_unaligned( A + (pos-32) );
+      else {
+        uint64_t mp = pos - 64;
+        if( mp + 8 <= sz ) v = fd_ld_u64_unaligned( M + mp );
+        else {
+          v = 0;
+          if( mp < sz ) {
+            uint64_t keep = sz - mp;                 /* 1..7 bytes of message */
+            v = fd_ld_u64_unaligned( M + mp ) & ((1ULL << (8*keep)) - 1ULL);
+          }
+          if( pos <= L && L < pos + 8 ) v |= 0x80ULL << (8*(L-pos));
+        }
+      }
+      uint64_t be = fd_bswap64( v );
+      if( b==nblk-1 && i==15 ) be = L << 3;        /* bit count, low 64 bits */
+      /* bit count high word (i==14) is 0 for any 32-bit sz */
+      w[i] = be;
+    }
+    fd_sha512_compress( st, w );
+  }
+#pragma unroll
+  for( int i=0; i<8; i++ ) dig[i] = fd_bswap64( st[i] );
+}
+
+/* fd_ed25519_sc_reduce: 512-bit little endian -> 256-bit mod L.
+   Input/outputs as little-endian 64-bit words. */
+#define FD_SC_FOLD(k) do { s[(k)-12] += s[k]*666643; s[(k)-11] += s[k]*470296; s[(k)-10] += s[k]*654183; \
+                           s[(k)-9]  -= s[k]*997805; s[(k)-8]  += s[k]*136657; s[(k)-7]  -= s[k]*683901; s[k] = 0; } while(0)
+#define FD_SC_CR(k) do { int64_t c_ = (s[k] + (1LL<<20)) >> 21; s[(k)+1] += c_; s[k] -= (int64_t)((uint64_t)c_ << 21); } while(0)
+#define FD_SC_CF(k) do { int64_t c_ = s[k] >> 21;               s[(k)+1] += c_; s[k] -= (int64_t)((uint64_t)c_ << 21); } while(0)
+
+FD_DEV void fd_sc_reduce( uint64_t (&out)[4], uint64_t const (&in)[8] ) {
+  int64_t s[24];
+  uint64_t const m = (1ULL<<21)-1ULL;
+#pragma unroll
+  for( int i=0; i<23; i++ ) {
+    int bit = 21*i, wd = bit>>6, sh = bit&63;
+    uint64_t v = in[wd] >> sh;
+    if( sh > 43 && wd+1 < 8 ) v |= in[wd+1] << (64-sh);
+    s[i] = (int64_t)(v & m);
+  }
+  s[23] = (int64_t)(in[7] >> 35);
+
+#pragma unroll
+  for( int k=23; k>=18; k-- ) FD_SC_FOLD(k);
+  FD_SC_CR(6); FD_SC_CR(8); FD_SC_CR(10); FD_SC_CR(12); FD_SC_CR(14); FD_SC_CR(16);
+  FD_SC_CR(7); FD_SC_CR(9); FD_SC_CR(11); FD_SC_CR(13); FD_SC_CR(15);
+#pragma unroll
+  for( int k=17; k>=12; k-- ) FD_SC_FOLD(k);
+  FD_SC_CR(0); FD_SC_CR(2); FD_SC_CR(4); FD_SC_CR(6); FD_SC_CR(8); FD_SC_CR(10);
+  FD_SC_CR(1); FD_SC_CR(3); FD_SC_CR(5); FD_SC_CR(7); FD_SC_CR(9); FD_SC_CR(11);
+  FD_SC_FOLD(12);
+#pragma unroll
+  for( int k=0; k<12; k++ ) FD_SC_CF(k);
+  FD_SC_FOLD(12);
+#pragma unroll
+  for( int k=0; k<11; k++ ) FD_SC_CF(k);
+
+  uint64_t u[12];
+#pragma unroll
+  for( int k=0; k<12; k++ ) u[k] = (uint64_t)s[k];
+  out[0] = (u[0]    ) | (u[1] <<21) | (u[2] <<42) | (u[3] <<63);
+  out[1] = (u[3] >>1) | (u[4] <<20) | (u[5] <<41) | (u[6] <<62);
+  out[2] = (u[6] >>2) | (u[7] <<19) | (u[8] <<40) | (u[9] <<61);
+  out[3] = (u[9] >>3) | (u[10]<<18) | (u[11]<<39);
+}
+
+#undef FD_SC_FOLD
+#undef FD_SC_CR
+#undef FD_SC_CF
+
+#endif /* FD_ED25519_GPU_SHA512_H */

@@ -1,0 +1,184 @@
+#ifndef HEADER_fd_ed25519_gpu_h
+#define HEADER_fd_ed25519_gpu_h
+
+/* fd_ed25519_gpu.h -- C ABI of the MI355X Ed25519 verification engine.
+
+   Drop-in boundary for tinydancer-io/firedancer's sigverify path
+   (SURVEY.md section 8b).  Every entry point takes plain pointers and
+   sizes; no HIP or torch types appear in a signature (streams are
+   passed as void *).  Result codes are the reference's
+   (src/ballet/ed25519/fd_ed25519.h:11-14) and every per-signature code
+   is bit-exact with the reference's AVX2 fd_ed25519_verify on the same
+   inputs.  The library fails loudly (FD_ED25519_ERR_GPU) when no
+   gfx950 device is usable; it has no CPU fallback. */
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Reference codes (fd_ed25519.h:11-14) */
+#define FD_ED25519_SUCCESS    ( 0) /* signature verified */
+#define FD_ED25519_ERR_SIG    (-1) /* signature obviously invalid (S >= L, small-order R) */
+#define FD_ED25519_ERR_PUBKEY (-2) /* public key invalid (or R not on curve) */
+#define FD_ED25519_ERR_MSG    (-3) /* equation mismatch */
+/* Engine codes (new; never produced by the reference) */
+#define FD_ED25519_ERR_ARG    (-16) /* malformed batch: offsets/lengths out of bounds */
+#define FD_ED25519_ERR_GPU    (-17) /* device/runtime failure; no result produced */
+
+#define FD_ED25519_SIG_SZ (64UL)
+
+/* ---- Per-signature API (replaces fd_ed25519.h:96-101) -----------------
+
+   fd_ed25519_verify verifies one signature on the process-default
+   engine (device from $FD_ED25519_GPU_DEVICE, default 0).  sha is the
+   reference's caller-owned fd_sha512_t scratch; it is accepted for ABI
+   compatibility and not touched.  msg==NULL is fine when sz==0. */
+
+int
+fd_ed25519_verify( void const *  msg,
+                   unsigned long sz,
+                   void const *  sig,
+                   void const *  public_key,
+                   void *        sha );
+
+/* fd_ed25519_strerror (fd_ed25519.h:108-109, fd_ed25519_user.c:435-445) */
+char const *
+fd_ed25519_strerror( int err );
+
+/* ---- Batch APIs (new) ---------------------------
+
+   fd_ed25519_verify_batch: out_err[i] = fd_ed25519_verify( msg[i],
+   msg_sz[i], sig[i], pub[i] ).  Returns 0 if every signature verified,
+   else the first nonzero code in index order.  Returns
+   FD_ED25519_ERR_ARG (and writes nothing) if n==0 with NULL arrays is
+   not the case and any array is NULL, or a msg_sz exceeds 2^31. */
+
+int
+fd_ed25519_verify_batch( unsigned long           n,
+                         uint8_t const * const * msg,
+                         unsigned long const *   msg_sz,
+                         uint8_t const * const * sig,
+                         uint8_t const * const * pub,
+                         int *                   out_err );
+
+/* fd_ed25519_verify_batch_single_msg: n signers over one shared message
+   (vote-txn shape).  Returns 0 iff every element verifies, else the
+   first nonzero code in index order.  out_err_opt may be NULL. */
+
+int
+fd_ed25519_verify_batch_single_msg( uint8_t const * msg,
+                                    unsigned long   msg_sz,
+                                    uint8_t const (*sig)[64],
+                                    uint8_t const (*pub)[32],
+                                    unsigned long   n,
+                                    int *           out_err_opt );
+
+/* ---- Engine (the util/gpu shim) ----------------------------------------
+
+   A packed batch is one byte blob plus one descriptor per signature
+   giving byte offsets into the blob: signature i is R||S at
+   blob[sig_off..+64), its public key at blob[pub_off..+32) and its
+   message at blob[msg_off..+msg_sz).  This matches a Solana txn payload
+   directly (signatures, account keys and message all live inside the
+   payload, src/ballet/txn/fd_txn.h:159-217), so a txn's bytes cross
+   PCIe once however many signatures it carries. */
+
+typedef struct fd_ed25519_gpu_desc {
+  uint32_t sig_off;
+  uint32_t pub_off;
+  uint32_t msg_off;
+  uint32_t msg_sz;
+} fd_ed25519_gpu_desc_t;
+
+typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
+
+/* Create an engine on HIP device `device` able to take batches of up to
+   max_sigs signatures and max_blob payload bytes.  All device memory,
+   pinned host rings and streams are allocated here (call before any
+   sandboxing).  Returns NULL on failure. */
+fd_ed25519_gpu_t *
+fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob );
+
+void
+fd_ed25519_gpu_delete( fd_ed25519_gpu_t * gpu );
+
+/* Synchronous: host blob/desc in, host codes out.  Bounds-checks every
+   descriptor (FD_ED25519_ERR_ARG in out[i] for a malformed one).
+   Returns 0 on success (codes in out) or FD_ED25519_ERR_GPU /
+   FD_ED25519_ERR_ARG if the batch could not be run. */
+int
+fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t *            gpu,
+                              unsigned long                 n,
+                              void const *                  blob,
+                              unsigned long                 blob_sz,
+                              fd_ed25519_gpu_desc_t const * desc,
+                              int *                         out );
+
+/* Device-resident: d_blob (padded by >= 16 readable bytes), d_desc and
+   d_out are device pointers; enqueued on `stream` (a hipStream_t, NULL
+   for the engine's own stream); no host synchronisation.  Descriptors
+   must already be in bounds. */
+int
+fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
+                           unsigned long                 n,
+                           void const *                  d_blob,
+                           fd_ed25519_gpu_desc_t const * d_desc,
+                           int *                         d_out,
+                           void *                        stream );
+
+/* Asynchronous pipeline over the engine's pinned host rings: submit
+   copies the batch into a free pinned slot and enqueues H2D copy,
+   kernels and D2H copy on that slot's stream; poll returns 1 and fills
+   out when the batch has completed, 0 if still in flight, <0 on error.
+   At most fd_ed25519_gpu_depth() batches may be outstanding. */
+int
+fd_ed25519_gpu_submit( fd_ed25519_gpu_t *            gpu,
+                       unsigned long                 n,
+                       void const *                  blob,
+                       unsigned long                 blob_sz,
+                       fd_ed25519_gpu_desc_t const * desc,
+                       unsigned long *               ticket );
+
+int
+fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
+                     unsigned long      ticket,
+                     int *              out,
+                     int                block );
+
+int
+fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
+
+/* Device the engine runs on; last HIP error string (diagnostics). */
+int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
+char const * fd_ed25519_gpu_last_error( void );
+
+/* Number of usable gfx950 devices visible to this process. */
+int fd_ed25519_gpu_device_cnt( void );
+
+/* ---- Test-data signer (CPU; not on the verify path) -------------------
+   fd_ed25519_public_from_private / fd_ed25519_sign as fd_ed25519.h:40-73:
+   RFC 8032 Ed25519.  Provided so benchmarks can build signed synthetic
+   corpora without the test oracle. */
+
+void * fd_ed25519_public_from_private( void * public_key, void const * private_key, void * sha );
+void * fd_ed25519_sign( void * sig, void const * msg, unsigned long sz, void const * public_key,
+                        void const * private_key, void * sha );
+
+/* Batch key derivation: pub[32i] from seed[32i]. */
+void fd_ed25519_public_batch( unsigned long n, uint8_t const * seed, uint8_t * pub, int nthreads );
+
+/* Batch signer: key i from seed[32i], message blob+msg_off[i] (msg_sz[i]),
+   writes pub[32i], sig[64i]; nthreads host threads.  With nthreads < 0,
+   pub[] is taken as input (keys already derived) and |nthreads| threads
+   are used. */
+void fd_ed25519_sign_batch( unsigned long n, uint8_t const * seed, uint8_t const * blob,
+                            uint64_t const * msg_off, uint32_t const * msg_sz,
+                            uint8_t * pub, uint8_t * sig, int nthreads );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_ed25519_gpu_h */
