@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""bench.py -- Ed25519 batch verification throughput on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): 4096-signature batches of
+Solana-MTU (1232-byte) legacy txn payloads with 1-2 signatures per txn
+(p = 0.7 / 0.3), all valid, synthetic (keys and messages from fixed
+seeds, signed by the product's host signer).  One step = one pass of the
+verify path over STEP_BATCHES such batches resident in HBM (one engine
+launch: prep -> decomp -> dsm).  value = signatures verified by all ranks
+/ max over ranks of the timed wall time (inputs already in HBM).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
+--gpus N): one process per GPU, each an independent replica on its own
+shard of signatures (no data-path collective -- nothing is reduced);
+RCCL only carries the timing barrier and the max-over-ranks.
+
+Extra measurements on rank 0 at N=1:
+  roofline     per-kernel HIP-event durations over the timed launches,
+               algorithmic int32 ops / duration
+  latency      submit -> results-on-host of single 4096-signature batches
+               through the pinned-ring pipeline (PCIe inclusive), p50/p99
+  cpu_baseline the reference's own fd_ed25519_verify (oracle/_ref build,
+               'reference') or the CPU restatement ('port') on a bounded
+               sample of the same corpus, all host threads of this rank
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BATCH_SIGS = 4096
+STEP_BATCHES = 64
+UNIQUE_SIGS = 65536
+
+# ---- algorithmic work model ----
+OPS_PER_FIELD_MUL = 490          # 10x10 schoolbook + carry chain, int32 ops
+OPS_PER_SHA_BLOCK = 4900         # 80 rounds + schedule, as 32-bit-pair ops
+FMUL_DSM = 2538                  # Ai table 96 + 251.5 dbl x 7 + 84.9 add x 8 + compare 2
+FMUL_DECOMP = 606                # 2 points x (pow22523 265 + 12 + small-order 26)
+PEAK_INT32_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 T/s
+
+
+def sha_blocks(msg_sz):
+    return (64 + msg_sz + 17 + 127) // 128
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--step-batches", type=int, default=STEP_BATCHES)
+    ap.add_argument("--unique", type=int, default=UNIQUE_SIGS)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--latency-batches", type=int, default=300)
+    ap.add_argument("--cpu-sample", type=int, default=196608, help="signatures in the CPU baseline sample")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, nsig, threads):
+    """Time the reference build (preferred) or the CPU restatement over a
+    bounded sample of the same corpus."""
+    import ctypes
+    ref = os.path.join(ROOT, "oracle", "_ref", "libfdref.so")
+    port = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(ref):
+        L, kind, fn = ctypes.CDLL(ref), "reference", "ref_verify_batch"
+    elif os.path.exists(port):
+        L, kind, fn = ctypes.CDLL(port), "port", "oracle_verify_batch"
+    else:
+        return None
+    sub = batch.tile(int(math.ceil(nsig / len(batch))))
+    sub.desc = sub.desc[:nsig]
+    sig, pub, data, off, sz = sub.flat()
+    out = np.zeros(nsig, np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    t0 = time.perf_counter()
+    getattr(L, fn)(ctypes.c_uint64(nsig), P(sig), P(pub), P(data), P(off), P(sz), P(out), threads)
+    dt = time.perf_counter() - t0
+    assert (out == 0).all(), "CPU baseline rejected valid signatures"
+    return {"value": nsig / dt, "unit": "verifies/s", "cores": threads, "kind": kind,
+            "sample": f"{nsig} signatures of the same C2 corpus (1232-byte txns, msg 1167/1103 B), "
+                      f"{threads} host threads, {dt:.2f} s wall ({dt * threads:.1f} thread-s)",
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    import firedancer_amd as fa
+    from firedancer_amd import corpus
+
+    n_step = a.step_batches * BATCH_SIGS
+    t0 = time.time()
+    base = corpus.solana_txns(a.unique, seed=1000 + rank, nthreads=min(16, os.cpu_count() or 8))
+    batch = base.tile(int(math.ceil(n_step / len(base))))
+    batch.desc = batch.desc[:n_step]
+    gen_s = time.time() - t0
+
+    eng = fa.Engine(local, max_sigs=max(n_step, 1 << 16), max_blob=max(len(batch.blob), 1 << 24))
+    dev = torch.device("cuda", local)
+    d_blob = torch.from_numpy(np.concatenate([batch.blob, np.zeros(64, np.uint8)])).to(dev)
+    d_desc = torch.from_numpy(batch.desc.view(np.uint8).copy()).to(dev)
+    d_out = torch.zeros(n_step, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        eng.verify_dev(n_step, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = bool((d_out == 0).all().item())
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    total = n_step * a.steps * world
+    value = total / elapsed
+    res = {
+        "metric": "Ed25519 verifies/sec at 1/2/4/8 MI355X; p99 latency per 4096-sig batch",
+        "value": value,
+        "unit": "verifies/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: 4096-signature batches of 1232-byte Solana legacy txns, 1-2 sigs/txn (p=0.7/0.3), all valid",
+            "batch_sigs": BATCH_SIGS,
+            "batches_per_step": a.step_batches,
+            "sigs_per_step_per_gpu": n_step,
+            "unique_sigs_per_gpu": len(base),
+            "msg_sz": sorted(set(int(x) for x in np.unique(base.desc["msg_sz"]))),
+            "parallelism": f"replicas x{world} (independent per-GPU shards, no collective)",
+        },
+        "all_accepted": ok,
+    }
+
+    if rank == 0 and world == 1:
+        # per-kernel durations over the same launches, on the launch stream
+        reps = max(3, min(a.steps, 10))
+        ks = np.zeros(3)
+        for _ in range(reps):
+            ks += eng.verify_dev_timed(n_step, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), stream)
+        ks /= reps
+        msz = base.desc["msg_sz"].astype(np.int64)
+        blocks = float(np.mean([sha_blocks(int(m)) for m in msz]))
+        ops = {"fd_k_prep": OPS_PER_SHA_BLOCK * blocks * n_step,
+               "fd_k_decomp": FMUL_DECOMP * OPS_PER_FIELD_MUL * n_step,
+               "fd_k_dsm": FMUL_DSM * OPS_PER_FIELD_MUL * n_step}
+        kern = {}
+        for name, ms in zip(fa.Engine.KERNELS, ks):
+            ach = ops[name] / (ms * 1e-3) / 1e12
+            kern[name] = {"ms": float(ms), "achieved_Tops": ach, "frac": ach * 1e12 / PEAK_INT32_OPS}
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        traffic = None
+        if os.path.exists(a.traffic):
+            try:
+                tr = json.load(open(a.traffic))
+                if tr.get("sigs_per_launch") == n_step:
+                    traffic = tr.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        w_total = (FMUL_DSM + FMUL_DECOMP) * OPS_PER_FIELD_MUL + OPS_PER_SHA_BLOCK * blocks
+        res["roofline"] = {
+            "bound": "valu-int32",
+            "kernel": dom,
+            "achieved": kern[dom]["achieved_Tops"],
+            "peak": PEAK_INT32_OPS / 1e12,
+            "unit": "Tint32op/s",
+            "frac": kern[dom]["frac"],
+            "traffic": traffic,
+            "per_kernel": kern,
+            "pipeline_frac": value * w_total / PEAK_INT32_OPS,
+            "ops_per_verify": w_total,
+        }
+        if not a.no_latency:
+            res["latency"] = latency(eng, base, a.latency_batches)
+        if not a.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, min(16, os.cpu_count() or 8))
+        res["corpus_gen_s"] = gen_s
+
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def latency(eng, base, nb):
+    """Single 4096-signature batches, host pinned ring -> GPU -> host,
+    depth-deep pipeline kept full; submit -> completion per batch."""
+    nb = max(nb, 20)
+    depth = eng.depth
+    starts = np.random.default_rng(7).integers(0, len(base) - BATCH_SIGS, nb)
+    # each batch: its own compacted blob (the txn payload bytes it references)
+    jobs = []
+    for s in starts[: min(nb, 64)]:
+        d = base.desc[s:s + BATCH_SIGS].copy()
+        lo = int(min(d["sig_off"].min(), d["pub_off"].min(), d["msg_off"].min()))
+        hi = int(max((d["msg_off"] + d["msg_sz"]).max(), d["sig_off"].max() + 64))
+        for f in ("sig_off", "pub_off", "msg_off"):
+            d[f] -= lo
+        jobs.append((np.ascontiguousarray(base.blob[lo:hi]), d))
+    out = np.zeros(BATCH_SIGS, np.int32)
+    lat = []
+    inflight = []
+    t_all = time.perf_counter()
+    for i in range(nb):
+        blob, d = jobs[i % len(jobs)]
+        if len(inflight) == depth:
+            t, ts = inflight.pop(0)
+            eng.poll(t, out, block=True)
+            lat.append(time.perf_counter() - ts)
+        ts = time.perf_counter()
+        inflight.append((eng.submit(blob, d), ts))
+    for t, ts in inflight:
+        eng.poll(t, out, block=True)
+        lat.append(time.perf_counter() - ts)
+    wall = time.perf_counter() - t_all
+    lat = np.array(lat[depth:]) * 1e3  # drop the ramp
+    return {"batch_sigs": BATCH_SIGS, "batches": nb, "pipeline_depth": depth,
+            "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall}
+
+
+if __name__ == "__main__":
+    main()

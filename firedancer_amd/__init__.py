@@ -34,12 +34,29 @@ class EngineError(RuntimeError):
     pass
 
 
+def _share_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own
+    libamdhip64 (soname libamdhip64.so.7) and links it by file name, so if
+    our library (which needs libamdhip64.so.7) were loaded first, torch
+    would later load a second runtime and fail to initialise the GPU.
+    Importing torch first makes the loader satisfy our dependency with
+    torch's already-loaded copy.  Without torch, /opt/rocm's runtime is
+    used."""
+    if os.environ.get("FD_ED25519_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load the product library (fails loudly when it was not built)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise EngineError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C firedancer_amd)")
+        _share_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         vp, ul, ip = ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int
         L.fd_ed25519_verify.argtypes = [vp, ul, vp, vp, vp]
@@ -58,6 +75,12 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_verify_packed.restype = ip
         L.fd_ed25519_gpu_verify_dev.argtypes = [vp, ul, vp, vp, vp, vp]
         L.fd_ed25519_gpu_verify_dev.restype = ip
+        L.fd_ed25519_gpu_verify_dev_timed.argtypes = [vp, ul, vp, vp, vp, vp, vp]
+        L.fd_ed25519_gpu_verify_dev_timed.restype = ip
+        L.fd_ed25519_gpu_kernel_cnt.argtypes = []
+        L.fd_ed25519_gpu_kernel_cnt.restype = ip
+        L.fd_ed25519_public_batch.argtypes = [ul, vp, vp, ip]
+        L.fd_ed25519_public_batch.restype = None
         L.fd_ed25519_gpu_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fd_ed25519_gpu_submit.restype = ip
         L.fd_ed25519_gpu_poll.argtypes = [vp, ul, vp, ip]
@@ -130,6 +153,16 @@ class Engine:
         err = lib().fd_ed25519_gpu_verify_dev(self._h, n, d_blob, d_desc, d_out, stream or None)
         if err:
             raise EngineError(f"verify_dev: {strerror(err)}: {last_error()}")
+
+    KERNELS = ("fd_k_prep", "fd_k_decomp", "fd_k_dsm")
+
+    def verify_dev_timed(self, n: int, d_blob: int, d_desc: int, d_out: int, stream: int = 0) -> np.ndarray:
+        """verify_dev with per-kernel HIP-event durations (ms), in KERNELS order."""
+        ms = np.zeros(lib().fd_ed25519_gpu_kernel_cnt(), np.float32)
+        err = lib().fd_ed25519_gpu_verify_dev_timed(self._h, n, d_blob, d_desc, d_out, stream or None, _p(ms))
+        if err:
+            raise EngineError(f"verify_dev_timed: {strerror(err)}: {last_error()}")
+        return ms
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
         t = ctypes.c_ulong(0)

@@ -201,7 +201,8 @@ def solana_txns(n_sigs, seed=0, p2=0.3, max_sigs_per_txn=2, nthreads=8, sig_dist
 
     payload = compact_u16(k) | k x sig | message, message =
       header(3) | compact_u16(m) | m x 32-byte account keys (signers first) |
-      blockhash(32) | compact_u16(1) | one instruction filling the MTU.
+      blockhash(32) | compact_u16(1) | one instruction whose data fills the
+      MTU.  Every txn parses with firedancer_amd.txn.parse.
     Signature j covers message = payload[1+64k:] with account key j.
     sig count: 1 or 2 with p(2)=p2, or drawn from sig_dist (list of
     probabilities for k = 1..len)."""
@@ -235,11 +236,19 @@ def solana_txns(n_sigs, seed=0, p2=0.3, max_sigs_per_txn=2, nthreads=8, sig_dist
         blob[mo + 3] = m
         for j in range(k):
             blob[mo + 4 + 32 * j: mo + 4 + 32 * (j + 1)] = pubs[s + j]
-        rest = mo + 4 + 32 * k
-        nb = (b + TXN_MTU) - rest
-        blob[rest:b + TXN_MTU] = filler[:nb]
+        rest = mo + 4 + 32 * m                  # after the account keys
+        blob[mo + 4 + 32 * k:rest] = filler[:32 * (m - k)]
+        blob[rest:rest + 32] = filler[32:64]    # recent blockhash
+        rest += 32
+        dl = b + TXN_MTU - (rest + 1 + 1 + 1 + 2)
+        blob[rest] = 1                          # one instruction
+        blob[rest + 1] = m - 1                  # program id index
+        blob[rest + 2] = 0                      # no account indices
+        blob[rest + 3] = 0x80 | (dl & 0x7F)     # compact-u16 data length
+        blob[rest + 4] = dl >> 7
+        blob[rest + 5:b + TXN_MTU] = filler[:dl]
         # unique per txn so no two messages collide
-        blob[rest:rest + 8] = np.frombuffer(np.uint64(t).tobytes(), np.uint8)
+        blob[rest + 5:rest + 13] = np.frombuffer(np.uint64(t).tobytes(), np.uint8)
         for j in range(k):
             desc[s + j] = (b + 1 + 64 * j, mo + 4 + 32 * j, mo, TXN_MTU - 1 - 64 * k)
             msg_off[s + j] = mo

@@ -47,6 +47,7 @@ struct fd_ed25519_gpu {
   unsigned long max_blob;
   unsigned long next_ticket;
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH];
+  hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
 };
 
@@ -118,6 +119,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
   }
+  for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
   return g;
 fail:
   fd_ed25519_gpu_delete( g );
@@ -140,6 +142,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     if( sl->stream ) hipStreamDestroy( sl->stream );
     if( sl->done   ) hipEventDestroy( sl->done );
   }
+  for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->kev[k] ) hipEventDestroy( g->kev[k] );
   delete g;
 }
 
@@ -166,6 +169,25 @@ extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n,
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   return 0;
 }
+
+extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob,
+                                                fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream,
+                                                float * kernel_ms ) {
+  if( !g || n > g->max_sigs || !kernel_ms ) return FD_ED25519_ERR_ARG;
+  hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev );
+  if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
+  if( (e = hipEventSynchronize( g->kev[FD_ED25519_GPU_KERNEL_CNT] )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+  for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
+    kernel_ms[k] = 0.f;
+    if( n && (e = hipEventElapsedTime( &kernel_ms[k], g->kev[k], g->kev[k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
+  }
+  return 0;
+}
+
+extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_CNT; }
 
 /* Stage a batch into a slot's pinned buffers and enqueue copy-in,
    kernels, copy-out on the slot's stream. */

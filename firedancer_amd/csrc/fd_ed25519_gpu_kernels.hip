@@ -403,13 +403,23 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
   return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_precomp), FD_GPU_BI_PRECOMP, sizeof(FD_GPU_BI_PRECOMP) );
 }
 
-extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
-                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream ) {
+extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                                    fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                                    hipEvent_t const * ev ) {
   if( !n ) return hipSuccess;
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)((2*n + 255) / 256);
+  if( ev ) hipEventRecord( ev[0], stream );
   hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->slides_k, w->slides_s );
+  if( ev ) hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts );
+  if( ev ) hipEventRecord( ev[2], stream );
   hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->slides_k, w->slides_s, w->tab, out );
+  if( ev ) hipEventRecord( ev[3], stream );
   return hipGetLastError();
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream ) {
+  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL );
 }

@@ -22,12 +22,18 @@ typedef struct fd_ed25519_gpu_work {
 } fd_ed25519_gpu_work_t;
 
 /* bytes of HBM working set per signature of capacity */
+/* number of kernels in one launch (timed API) */
+#define FD_ED25519_GPU_KERNEL_CNT 3
+
 #define FD_ED25519_GPU_WORK_PER_SIG (4UL + 512UL + 8UL + 320UL + 1280UL)
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 hipError_t fd_ed25519_gpu_upload_tables( void );
+hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                        fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                        hipEvent_t const * ev );
 hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream );
 #ifdef __cplusplus

@@ -150,6 +150,23 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 
+/* Diagnostics: fd_ed25519_gpu_verify_dev with HIP events around each of
+   the engine's fd_ed25519_gpu_kernel_cnt() kernels on `stream`; blocks
+   until done and writes each kernel's duration (ms) to kernel_ms[].
+   Kernel order: prep (SHA-512, mod L, recoding), decomp (point
+   decompression + small-order test), dsm (double-scalar multiplication
+   + compare). */
+int
+fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t *            gpu,
+                                 unsigned long                 n,
+                                 void const *                  d_blob,
+                                 fd_ed25519_gpu_desc_t const * d_desc,
+                                 int *                         d_out,
+                                 void *                        stream,
+                                 float *                       kernel_ms );
+
+int fd_ed25519_gpu_kernel_cnt( void );
+
 /* Device the engine runs on; last HIP error string (diagnostics). */
 int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
 char const * fd_ed25519_gpu_last_error( void );

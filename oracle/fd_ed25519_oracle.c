@@ -153,16 +153,15 @@ EXPORT void oracle_sc_reduce( u8 const * in, u8 * out ) {
   SC_FOLD( s[12], 12 );
   for( int k=0; k<11; k++ ) SC_CARRY_F(k);
 
-  /* pack 12 x 21 bits little endian */
-  memset( out, 0, 32 );
-  for( int k=0; k<12; k++ ) {
-    u64 v = (u64)s[k];
-    for( int b=0; b<21; b++ ) {
-      int bit = 21*k + b;
-      if( bit >= 256 ) break;
-      if( (v>>b) & 1 ) out[bit>>3] |= (u8)(1u << (bit&7));
-    }
-  }
+  /* pack as the reference does (fd_ed25519_user.c:105-108): limb 11 may
+     carry bit 252 above its 21 bits */
+  u64 u[12]; for( int k=0; k<12; k++ ) u[k] = (u64)s[k];
+  u64 w[4];
+  w[0] = (u[0]    ) | (u[1] <<21) | (u[2] <<42) | (u[3] <<63);
+  w[1] = (u[3] >>1) | (u[4] <<20) | (u[5] <<41) | (u[6] <<62);
+  w[2] = (u[6] >>2) | (u[7] <<19) | (u[8] <<40) | (u[9] <<61);
+  w[3] = (u[9] >>3) | (u[10]<<18) | (u[11]<<39);
+  for( int i=0; i<4; i++ ) for( int j=0; j<8; j++ ) out[8*i+j] = (u8)(w[i] >> (8*j));
 }
 
 /* ---------------------------------------------------------------- */

@@ -1,0 +1,177 @@
+"""GPU parity: every per-signature code of the engine equals the
+reference's (AVX2 fd_ed25519_verify) on the same inputs.
+
+Checkers: the committed golden corpora (expected codes produced by the
+reference build), the reference build itself when it was shipped with
+the tree (oracle/_ref/libfdref.so), and the CPU restatement
+(oracle/liboracle.so).  Full BASELINE sizes are covered through
+size-independent properties (all-valid => all accept, permutation
+equivariance, repeatability, corruption => reject)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import firedancer_amd as fa
+from conftest import ROOT, ed_vectors, load_corpus, malleability, oracle_batch
+from firedancer_amd import corpus, txn
+
+pytestmark = pytest.mark.gpu
+
+
+def _checker(oracle):
+    path = os.path.join(ROOT, "oracle", "_ref", "libfdref.so")
+    return ctypes.CDLL(path) if os.path.exists(path) else oracle
+
+
+@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
+def test_golden_corpora(engine, name):
+    b, exp = load_corpus(name)
+    got = engine.verify_packed(b.blob, b.desc)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_vectors_rfc8032_and_q2(engine):
+    vs = ed_vectors()
+    b = corpus.from_triples([(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in vs])
+    got = engine.verify_packed(b.blob, b.desc)
+    assert got.tolist() == [v["expected"] for v in vs]
+    # the three Q2 vectors are valid RFC 8032 signatures the reference rejects
+    assert got[-3:].tolist() == [-3, -3, -3]
+
+
+def test_malleability_kats(engine):
+    m = malleability()
+    b = corpus.from_triples([(b"Zcash", s, p) for s, p, _ in m])
+    got = engine.verify_packed(b.blob, b.desc)
+    for (s, p, ok), g in zip(m, got):
+        assert (g == 0) == ok
+
+
+def test_txn_fixtures(engine):
+    from conftest import GOLDEN
+    parts, descs, off = [], [], 0
+    for i in (1, 2, 3):
+        p = open(os.path.join(GOLDEN, f"transaction{i}.bin"), "rb").read()
+        descs.append(txn.descs_for(p, off))
+        parts.append(p)
+        off += len(p)
+    blob = np.frombuffer(b"".join(parts) + b"\0" * 64, np.uint8).copy()
+    got = engine.verify_packed(blob, np.concatenate(descs))
+    assert got.tolist() == [0] * 6
+
+
+def test_adversarial_vs_reference(engine, oracle):
+    """C3 shape at 64K signatures, 10% invalid, checked signature by
+    signature against the reference build (or the restatement)."""
+    chk = _checker(oracle)
+    b = corpus.adversarial(65536, 128, seed=2024, invalid_frac=0.1)
+    exp = oracle_batch(chk, b)
+    got = engine.verify_packed(b.blob, b.desc)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), corpus.CASES[b.label[i]], int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_txn_mtu_batches_vs_reference(engine, oracle):
+    """C2 shape: 4096-signature batches of 1232-byte txns, 1-2 sigs each,
+    with 5% of signatures corrupted."""
+    chk = _checker(oracle)
+    b = corpus.solana_txns(4096 * 4, seed=77)
+    rng = np.random.default_rng(5)
+    for i in rng.choice(len(b), len(b) // 20, replace=False):
+        b.blob[int(b.desc[i]["sig_off"]) + rng.integers(0, 64)] ^= np.uint8(1 << rng.integers(0, 8))
+    exp = oracle_batch(chk, b)
+    got = engine.verify_packed(b.blob, b.desc)
+    assert (got == exp).all()
+    assert (exp != 0).sum() > 0
+
+
+def test_full_size_properties(engine):
+    """BASELINE C2 at full batch size (64 x 4096 signatures): all valid
+    => all accepted; permuting descriptors permutes results; two runs
+    agree; flipping one byte of each of 512 signatures rejects them."""
+    base = corpus.solana_txns(16384, seed=31)
+    b = base.tile(16)
+    got = engine.verify_packed(b.blob, b.desc)
+    assert (got == 0).all()
+    perm = np.random.default_rng(1).permutation(len(b))
+    got_p = engine.verify_packed(b.blob, b.desc[perm])
+    assert (got_p == got[perm]).all()
+    blob = base.blob.copy()
+    idx = np.random.default_rng(2).choice(len(base), 512, replace=False)
+    for i in idx:
+        blob[int(base.desc[i]["sig_off"]) + 40] ^= 0x01   # S byte 8
+    got2 = engine.verify_packed(blob, base.desc)
+    assert (got2[idx] != 0).all()
+    mask = np.ones(len(base), bool)
+    mask[idx] = False
+    # only the corrupted signatures (and co-signers sharing nothing) change
+    assert (got2[mask] == 0).all()
+
+
+def test_empty_and_single(engine):
+    out = engine.verify_packed(np.zeros(64, np.uint8), np.zeros(0, fa.DESC_DTYPE))
+    assert len(out) == 0
+    b = corpus.simple(1, 0, seed=3)
+    assert engine.verify_packed(b.blob, b.desc).tolist() == [0]
+
+
+def test_malformed_descriptors(engine):
+    b = corpus.simple(8, 64, seed=4)
+    d = b.desc.copy()
+    d[3]["msg_sz"] = 1 << 30          # message runs past the blob
+    d[5]["sig_off"] = len(b.blob)      # signature outside the blob
+    got = engine.verify_packed(b.blob, d)
+    assert got[3] == fa.ERR_ARG and got[5] == fa.ERR_ARG
+    assert (np.delete(got, [3, 5]) == 0).all()
+
+
+def test_reference_shaped_apis(engine):
+    """fd_ed25519_verify, fd_ed25519_verify_batch and
+    fd_ed25519_verify_batch_single_msg on the process-default engine."""
+    b = corpus.adversarial(600, 100, seed=8, invalid_frac=0.3)
+    exp = engine.verify_packed(b.blob, b.desc)
+    msgs = [b.msg(i) for i in range(len(b))]
+    sigs = [b.sig(i) for i in range(len(b))]
+    pubs = [b.pub(i) for i in range(len(b))]
+    r, out = fa.verify_batch(msgs, sigs, pubs)
+    assert (out == exp).all()
+    first = exp[exp != 0]
+    assert r == (int(first[0]) if len(first) else 0)
+    for i in range(0, 600, 37):
+        assert fa.verify(msgs[i], sigs[i], pubs[i]) == exp[i]
+    # vote-shaped: many signers over one 442-byte message (transaction2 size)
+    sb, msg, sig, pub = corpus.single_msg(4096, 442, seed=9)
+    r, out = fa.verify_batch_single_msg(bytes(msg), sig, pub)
+    assert r == 0 and (out == 0).all()
+    sig2 = sig.copy()
+    sig2[100, 0] ^= 1
+    r, out = fa.verify_batch_single_msg(bytes(msg), sig2, pub)
+    assert out[100] != 0 and r == out[100] and (np.delete(out, 100) == 0).all()
+
+
+def test_async_ring(engine):
+    """submit/poll over the pinned ring: depth batches in flight, each
+    result identical to the synchronous path."""
+    bs = [corpus.adversarial(2048, 128, seed=40 + k, invalid_frac=0.2) for k in range(engine.depth)]
+    exp = [engine.verify_packed(b.blob, b.desc) for b in bs]
+    tickets = [engine.submit(b.blob, b.desc) for b in bs]
+    for t, b, e in zip(tickets, bs, exp):
+        out = np.zeros(len(b), np.int32)
+        assert engine.poll(t, out, block=True)
+        assert (out == e).all()
+
+
+def test_device_resident(engine):
+    """verify_dev on torch-allocated HBM (the bench's path)."""
+    torch = pytest.importorskip("torch")
+    b = corpus.adversarial(4096, 128, seed=12, invalid_frac=0.2)
+    exp = engine.verify_packed(b.blob, b.desc)
+    blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).cuda()
+    desc = torch.from_numpy(b.desc.view(np.uint8).copy()).cuda()
+    out = torch.zeros(len(b), dtype=torch.int32, device="cuda")
+    engine.verify_dev(len(b), blob.data_ptr(), desc.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == exp).all()
