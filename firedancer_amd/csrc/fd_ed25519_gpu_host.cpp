@@ -80,8 +80,8 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
   w->pts      = (int32_t *)p; p +=  320UL * N;
   w->status   = (int32_t *)p; p +=    4UL * N;
   w->pstat    = (int32_t *)p; p +=    8UL * N;
-  w->slides_k = (int8_t  *)p; p +=  256UL * N;
-  w->slides_s = (int8_t  *)p; p +=  256UL * N;
+  w->op_start = (int32_t *)p; p +=    4UL * N;
+  w->ops      = (uint8_t *)p; p += (unsigned long)FD_OPS_MAX * N;
 }
 
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob ) {

@@ -37,6 +37,11 @@ typedef fd_gpu_fe4_t fe4;
 
 __constant__ static fe4 fd_gpu_bi_precomp[8];
 
+/* minimum waves per SIMD requested for fd_k_dsm (caps its VGPRs) */
+#ifndef FD_DSM_WAVES
+#define FD_DSM_WAVES 3
+#endif
+
 /* ------------------------------------------------------------------ */
 /* 4-lane vector helpers: the AVX path's wl_t x 10 state, one field
    element per lane (fd_ed25519_fe_avx.h:32-69). */
@@ -95,36 +100,44 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
   for( int i=0; i<8; i++ ) w[i] = fd_ld_u32_unaligned( p + 4*i );
 }
 
-/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) streamed out as
-   signed digits, kept as a 256-bit running value V: a digit absorbing
-   bit i+b by subtraction is the reference's carry loop, i.e. V += 2^(i+b). */
-FD_DEV void fd_slide_write( uint64_t (&a)[4], int8_t * out, uint64_t stride ) {
-  /* V: 5 words so carries past bit 255 are kept (and ignored) */
-  uint64_t V[5] = { a[0], a[1], a[2], a[3], 0 };
-  for( int i=0; i<256; i++ ) {
-    int d = (int)((V[i>>6] >> (i&63)) & 1ULL);
-    if( d ) {
-      for( int b=1; b<=6 && i+b<256; b++ ) {
-        int p = i+b;
-        if( !((V[p>>6] >> (p&63)) & 1ULL) ) continue;
-        int up = 1 << b;
-        if( d + up <= 15 ) {
-          d += up; V[p>>6] &= ~(1ULL << (p&63));
-        } else if( d - up >= -15 ) {
-          d -= up;
-          /* add 2^p to V (bit p is set): ripple-carry over words */
-          int wd = p>>6; uint64_t add = 1ULL << (p&63);
-          for( int k=wd; k<5; k++ ) { uint64_t o = V[k]; V[k] = o + add; add = (V[k] < o) ? 1ULL : 0ULL; if( !add ) break; }
-        } else break;
-      }
+/* One position of fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400).
+   The scalar is kept as a 320-bit running value V; a digit that absorbs
+   bit p by subtraction is the reference's carry loop, i.e. V += 2^p.
+   Digit i is final once position i has been processed (later positions
+   only touch higher bits), so digits are consumed low to high. */
+FD_DEV int fd_slide_step( uint64_t (&V)[5], int i ) {
+  int d = (int)((V[i>>6] >> (i&63)) & 1ULL);
+  if( d ) {
+    for( int b=1; b<=6 && i+b<256; b++ ) {
+      int p = i+b;
+      if( !((V[p>>6] >> (p&63)) & 1ULL) ) continue;
+      int up = 1 << b;
+      if( d + up <= 15 ) {
+        d += up; V[p>>6] &= ~(1ULL << (p&63));
+      } else if( d - up >= -15 ) {
+        d -= up;
+        /* add 2^p to V (bit p is set): ripple-carry over words */
+        int wd = p>>6; uint64_t add = 1ULL << (p&63);
+        for( int k=wd; k<5; k++ ) { uint64_t o = V[k]; V[k] = o + add; add = (V[k] < o) ? 1ULL : 0ULL; if( !add ) break; }
+      } else break;
     }
-    out[ (uint64_t)i*stride ] = (int8_t)d;
   }
+  return d;
+}
+
+/* Op encoding of the DSM's per-lane op stream (see fd_k_dsm):
+     0x00                      D: doubling step
+     0x80 | t<<6 | neg<<5 | e  A: add (t=0: Ai table of -A, t=1: Bi table),
+                                  digit = (neg ? -1 : 1) * (2e+1) */
+#define FD_OP_ADD 0x80
+FD_DEV uint8_t fd_op_enc( int tbl, int d ) {
+  int a = d < 0 ? -d : d;
+  return (uint8_t)(FD_OP_ADD | (tbl << 6) | ((d < 0) << 5) | (a >> 1));
 }
 
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-           int32_t * __restrict__ status, int8_t * __restrict__ slides_k, int8_t * __restrict__ slides_s ) {
+           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
@@ -149,15 +162,31 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t 
     }
   }
   status[i] = st;
-  if( st != FD_ST_PENDING ) return;
+  if( st != FD_ST_PENDING ) { op_start[i] = FD_OPS_MAX; return; }
 
   uint64_t dig[8];
   fd_sha512_ram( dig, R, A, M, d.msg_sz );
   uint64_t k[4];
   fd_sc_reduce( k, dig );
-  fd_slide_write( k, slides_k + i, n );
-  uint64_t s[4] = { ((uint64_t)sw[1]<<32)|sw[0], ((uint64_t)sw[3]<<32)|sw[2], ((uint64_t)sw[5]<<32)|sw[4], ((uint64_t)sw[7]<<32)|sw[6] };
-  fd_slide_write( s, slides_s + i, n );
+
+  /* Recode k and S (slide) and emit the DSM op stream back to front: the
+     stream for bit i is D, then an add for k's digit, then one for S's
+     (avx/fd_ed25519_ge.c:490-523), for bits 255 down to 0.  Streams are
+     right-aligned at FD_OPS_MAX so all lanes of a wave finish on the same
+     step; fd_k_dsm reads the gap before op_start as D, an exact no-op on
+     the identity. */
+  uint64_t Vk[5] = { k[0], k[1], k[2], k[3], 0 };
+  uint64_t Vs[5] = { ((uint64_t)sw[1]<<32)|sw[0], ((uint64_t)sw[3]<<32)|sw[2],
+                     ((uint64_t)sw[5]<<32)|sw[4], ((uint64_t)sw[7]<<32)|sw[6], 0 };
+  int pos = FD_OPS_MAX - 1;
+  for( int b=0; b<256; b++ ) {
+    int da = fd_slide_step( Vk, b );
+    int db = fd_slide_step( Vs, b );
+    if( db ) { ops[(uint64_t)pos*n + i] = fd_op_enc( 1, db ); pos--; }
+    if( da ) { ops[(uint64_t)pos*n + i] = fd_op_enc( 0, da ); pos--; }
+    ops[(uint64_t)pos*n + i] = 0; pos--;
+  }
+  op_start[i] = pos + 1;
 }
 
 /* ------------------------------------------------------------------ */
@@ -298,29 +327,52 @@ FD_DEV void fd_tab_load( fe4 & v, int32_t const * tab, uint64_t n, uint64_t i, i
     for( int k=0; k<10; k++ ) v.l[l].v[k] = tab[((uint64_t)(e*40 + l*10 + k))*n + i];
 }
 
-extern "C" __global__ void __launch_bounds__(256)
+FD_DEV int fd_wave_min( int x ) {
+#pragma unroll
+  for( int o=32; o>0; o>>=1 ) { int y = __shfl_xor( x, o, 64 ); x = y < x ? y : x; }
+  return x;
+}
+
+/* p1p1 -> p3 conversion, lanes [Z, Y, X, T] = [t2*t3, t1*t2, t0*t3, t0*t1]:
+   operand for operand the reference's MUL(perm(vt,2,1,0,0),
+   perm(vt,3,2,3,1)) (avx/fd_ed25519_ge.c:506-508); its lanes Z, Y, X are
+   also the p1p1 -> p2 conversion MUL(vt, perm(vt,3,2,3,3)) (:521-522). */
+FD_DEV void fd_conv( fe4 & q, fe4 const & t ) {
+  fd_fe_mul( q.l[0], t.l[2], t.l[3] );
+  fd_fe_mul( q.l[1], t.l[1], t.l[2] );
+  fd_fe_mul( q.l[2], t.l[0], t.l[3] );
+  fd_fe_mul( q.l[3], t.l[0], t.l[1] );
+}
+
+extern "C" __global__ void __launch_bounds__(256, FD_DSM_WAVES)
 fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
-          int32_t const * __restrict__ pts, int8_t const * __restrict__ slides_k, int8_t const * __restrict__ slides_s,
+          int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
           int32_t * __restrict__ tab, int32_t * __restrict__ out ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= n ) return;
+  /* lanes past n stay in the wave (the step loop is wave-uniform) but
+     read item 0 and store nothing */
+  int live = i < n;
+  uint64_t ii = live ? i : 0;
   uint64_t m = 2*n;
-  int st = status[i];
-  if( st != FD_ST_PENDING ) { out[i] = st; return; }
-  int pa = pstat[i], pr = pstat[n+i];
-  /* error precedence (fd_ed25519_user.c:401-403) */
-  if( pa == FD_PT_BAD || pr == FD_PT_BAD ) { out[i] = FD_ED25519_ERR_PUBKEY; return; }
-  if( pa == FD_PT_SMALL ) { out[i] = FD_ED25519_ERR_PUBKEY; return; }
-  if( pr == FD_PT_SMALL ) { out[i] = FD_ED25519_ERR_SIG;    return; }
+  int st = status[ii];
+  int pa = pstat[ii], pr = pstat[n+ii];
+  int code;
+  /* error precedence (fd_ed25519_user.c:372-403) */
+  if( st != FD_ST_PENDING )                        code = st;
+  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
+  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
+  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
+  else                                             code = FD_ST_PENDING;
+  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
 
   fe4 vr, vt, vu;
   /* vr = [Z, Y, X, T] of -A (fd_ed25519_user.c:408-409 negates X, T) */
 #pragma unroll
   for( int k=0; k<10; k++ ) {
-    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + i]);
-    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + i];
-    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + i];
-    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + i]);
+    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + ii]);
+    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + ii];
+    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + ii];
+    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + ii]);
   }
 
   /* Ai = {A,3A,...,15A} cached (avx/fd_ed25519_ge.c:423-481) */
@@ -329,8 +381,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
   d111.l[3] = FD_GPU_D2;
   v_mul( vu, vr, d111 ); v_subadd_12( vu );
-  fd_tab_store( tab, n, i, 0, vu );
-  /* A2 = dbl(A): vt = perm(vr,2,1,2,0) + [Y,0,0,0] -> [X+Y, Y, X, Z] */
+  fd_tab_store( tab, n, ii, 0, vu );
   v_p2_dbl( vt, vr.l[2], vr.l[1], vr.l[0] );
   {
     fe4 a, b;   /* vr = MUL(perm(vt,3,2,3,1), perm(vt,2,1,0,0)) */
@@ -347,45 +398,83 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
     b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
     v_mul( vt, a, b );
     v_mul( vu, vt, d111 ); v_subadd_12( vu );
-    fd_tab_store( tab, n, i, e+1, vu );
+    fd_tab_store( tab, n, ii, e+1, vu );
   }
 
-  /* main loop (avx/fd_ed25519_ge.c:483-523); leading iterations on the
-     identity are exact no-ops (doubling (0:1:1) returns the same limbs),
-     so every lane runs the full 256 bits. */
-  fe X, Y, Z;
-  fd_fe_set( X, 0 ); fd_fe_set( Y, 1 ); fd_fe_set( Z, 1 );
-  for( int b=255; b>=0; b-- ) {
-    v_p2_dbl( vt, X, Y, Z );
-    for( int j=0; j<2; j++ ) {
-      int sl = j ? (int)slides_s[(uint64_t)b*n + i] : (int)slides_k[(uint64_t)b*n + i];
-      if( sl ) {
-        fe4 a, c;   /* p1p1 -> p3: MUL(perm(vt,2,1,0,0), perm(vt,3,2,3,1)) */
-        a.l[0]=vt.l[2]; a.l[1]=vt.l[1]; a.l[2]=vt.l[0]; a.l[3]=vt.l[0];
-        c.l[0]=vt.l[3]; c.l[1]=vt.l[2]; c.l[2]=vt.l[3]; c.l[3]=vt.l[1];
-        v_mul( vt, a, c );
-        int e = (sl < 0 ? -sl : sl) >> 1;
-        if( j ) vu = fd_gpu_bi_precomp[e];
-        else    fd_tab_load( vu, tab, n, i, e );
-        if( sl < 0 ) { fe t = vu.l[1]; vu.l[1] = vu.l[2]; vu.l[2] = t; }
-        v_subadd_12( vt );
-        v_mul( vt, vt, vu );
-        v_sub_mix( vt );
-        if( sl > 0 ) { fe t = vt.l[2]; vt.l[2] = vt.l[3]; vt.l[3] = t; }
+  /* Main loop as a per-lane op stream (avx/fd_ed25519_ge.c:488-523
+     restated).  Every step converts the p1p1 state to p3 (4 multiplies)
+     and applies its op -- D: DBL_MIX(SQN([X+Y,Y,X,Z]; 1,1,1,2)), the
+     squarings issued as multiplies f*f and Z*(2Z) (identical column sums
+     for these operand ranges); A:
+     SUB_MIX(MUL(SUBADD_12(p3), entry)) with the entry's lanes 1,2
+     swapped for a negative digit and the result's lanes 2,3 swapped for
+     a positive one.  All lanes run the same instructions on different
+     operands.  The initial p1p1 [0,1,1,1] converts to the identity. */
+#pragma unroll
+  for( int l=0; l<4; l++ ) fd_fe_set( vt.l[l], l ? 1 : 0 );
+  int t0 = fd_wave_min( start );
+  for( int t=t0; t<FD_OPS_MAX; t++ ) {
+    int op = (t >= start) ? (int)ops[(uint64_t)t*n + ii] : 0;
+    int is_add = op & FD_OP_ADD;
+    int e   = op & 7;
+    int neg = (op >> 5) & 1;
+    fe4 q; fd_conv( q, vt );   /* q = [Z, Y, X, T] */
+    /* operands of the op's four multiplies, built lane by lane; the table
+       entry is read lane by lane by add steps only (the Ai table does not
+       fit the caches at full batch size, so D steps must not touch it) */
+    int tb = op & 0x40;
+    int32_t const * trow = tab + (uint64_t)(e*40)*n + ii;
+    fe4 h;
+#pragma unroll
+    for( int l=0; l<4; l++ ) {
+      /* entry lane: lanes 1,2 swapped for a negative digit */
+      int el = (l==1 || l==2) ? (neg ? 3-l : l) : l;
+      fe ent;
+      if( tb ) ent = fd_gpu_bi_precomp[e].l[el];
+      else if( is_add ) {
+#pragma unroll
+        for( int k=0; k<10; k++ ) ent.v[k] = trow[(uint64_t)(el*10 + k)*n];
+      } else fd_fe_set( ent, 0 );
+      fe f, g;
+#pragma unroll
+      for( int k=0; k<10; k++ ) {
+        uint32_t z = q.l[0].v[k], y = q.l[1].v[k], x = q.l[2].v[k], t = q.l[3].v[k];
+        uint32_t fa, fd, gd;
+        if( l==0 ) { fa = z;   fd = x+y; gd = x+y;  }
+        if( l==1 ) { fa = y-x; fd = y;   gd = y;    }
+        if( l==2 ) { fa = y+x; fd = x;   gd = x;    }
+        if( l==3 ) { fa = t;   fd = z;   gd = 2u*z; }
+        f.v[k] = (int32_t)(is_add ? fa : fd);
+        g.v[k] = is_add ? ent.v[k] : (int32_t)gd;
       }
+      fd_fe_mul( h.l[l], f, g );
     }
-    /* p1p1 -> p2: MUL(vt, perm(vt,3,2,3,3)) */
-    fd_fe_mul( X, vt.l[0], vt.l[3] );
-    fd_fe_mul( Y, vt.l[1], vt.l[2] );
-    fd_fe_mul( Z, vt.l[2], vt.l[3] );
+    /* D: [a-b-c, b+c, b-c, d-b+c]; A: [c-b, c+b, 2a-d, 2a+d] with lanes
+       2,3 swapped for a positive digit */
+    int pos = is_add && !neg;
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      uint32_t a=h.l[0].v[k], b=h.l[1].v[k], c=h.l[2].v[k], d=h.l[3].v[k];
+      uint32_t d0 = a-b-c, d1 = b+c, d2 = b-c, d3 = d-b+c;
+      uint32_t a0 = c-b,   a1 = c+b, a2 = 2u*a-d, a3 = 2u*a+d;
+      vt.l[0].v[k] = (int32_t)(is_add ? a0 : d0);
+      vt.l[1].v[k] = (int32_t)(is_add ? a1 : d1);
+      vt.l[2].v[k] = (int32_t)(is_add ? (pos ? a3 : a2) : d2);
+      vt.l[3].v[k] = (int32_t)(is_add ? (pos ? a2 : a3) : d3);
+    }
   }
+  /* final p1p1 -> p2 */
+  fe X, Y, Z;
+  fd_fe_mul( X, vt.l[0], vt.l[3] );
+  fd_fe_mul( Y, vt.l[1], vt.l[2] );
+  fd_fe_mul( Z, vt.l[2], vt.l[3] );
 
   /* compare r.x*R.Z == R.X and r.y*R.Z == R.Y on limbs 0..7 (Q2) */
   fe rx, ry;
 #pragma unroll
   for( int k=0; k<10; k++ ) {
-    rx.v[k] = pts[(uint64_t)( 0+k)*m + n + i];
-    ry.v[k] = pts[(uint64_t)(10+k)*m + n + i];
+    rx.v[k] = pts[(uint64_t)( 0+k)*m + n + ii];
+    ry.v[k] = pts[(uint64_t)(10+k)*m + n + ii];
   }
   fe xz, yz;
   fd_fe_mul( xz, Z, rx );
@@ -393,7 +482,8 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   int eq = 1;
 #pragma unroll
   for( int k=0; k<8; k++ ) eq &= (xz.v[k] == X.v[k]) & (yz.v[k] == Y.v[k]);
-  out[i] = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if( code == FD_ST_PENDING ) code = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if( live ) out[i] = code;
 }
 
 /* ------------------------------------------------------------------ */
@@ -410,11 +500,11 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)((2*n + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
-  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->slides_k, w->slides_s );
+  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start );
   if( ev ) hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts );
   if( ev ) hipEventRecord( ev[2], stream );
-  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->slides_k, w->slides_s, w->tab, out );
+  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out );
   if( ev ) hipEventRecord( ev[3], stream );
   return hipGetLastError();
 }

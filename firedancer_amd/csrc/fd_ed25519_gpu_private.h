@@ -7,15 +7,15 @@
 
 /* Per-batch HBM working set, SoA [field][item] (sizes for capacity N):
      status   int32 [N]          prep result (S check) or pending
-     slides_k int8  [256][N]     signed window digits of k
-     slides_s int8  [256][N]     signed window digits of S
+     ops      uint8 [768][N]     per-signature DSM op stream, right aligned
+     op_start int32 [N]          first op index (FD_OPS_MAX if none)
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
      tab      int32 [320][N]     per-signature Ai table (8 x 4 lanes x 10) */
 typedef struct fd_ed25519_gpu_work {
   int32_t * status;
-  int8_t  * slides_k;
-  int8_t  * slides_s;
+  uint8_t * ops;
+  int32_t * op_start;
   int32_t * pstat;
   int32_t * pts;
   int32_t * tab;
@@ -25,7 +25,10 @@ typedef struct fd_ed25519_gpu_work {
 /* number of kernels in one launch (timed API) */
 #define FD_ED25519_GPU_KERNEL_CNT 3
 
-#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 512UL + 8UL + 320UL + 1280UL)
+/* op stream capacity: 256 doublings + at most 256 adds per scalar */
+#define FD_OPS_MAX 768
+
+#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 4UL + (unsigned long)FD_OPS_MAX + 8UL + 320UL + 1280UL)
 
 #ifdef __cplusplus
 extern "C" {
