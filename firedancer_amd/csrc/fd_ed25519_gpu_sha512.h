@@ -29,81 +29,114 @@ __constant__ static uint64_t const fd_gpu_sha512_k[80] = {
   0x431d67c49c100d4cULL,0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL
 };
 
-FD_DEV uint64_t fd_rotr64( uint64_t x, int n ) { return (x >> n) | (x << (64-n)); }
+/* 64-bit rotates/shifts as two full-rate v_alignbit_b32 (a 64-bit shift
+   pair would be two half-rate ops plus an or). n is a constant. */
+FD_DEV uint64_t fd_rotr64( uint64_t x, int n ) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if( n >= 32 ) { uint32_t t = lo; lo = hi; hi = t; n -= 32; }
+  if( !n ) return ((uint64_t)hi << 32) | lo;
+  uint32_t nlo = __builtin_amdgcn_alignbit( hi, lo, (uint32_t)n );
+  uint32_t nhi = __builtin_amdgcn_alignbit( lo, hi, (uint32_t)n );
+  return ((uint64_t)nhi << 32) | nlo;
+}
+FD_DEV uint64_t fd_shr64( uint64_t x, int n ) {   /* 0 < n < 32 */
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit( hi, lo, (uint32_t)n );
+}
 FD_DEV uint64_t fd_bswap64( uint64_t x ) { return __builtin_bswap64( x ); }
 
-/* 4 bytes at an arbitrary byte address, little endian; reads the
-   enclosing aligned words (the batch blob is padded by >= 16 bytes). */
+/* 4 bytes at an arbitrary byte address, little endian, from the two
+   enclosing aligned dwords (the batch blob is padded by >= 16 bytes).
+   Pointer arithmetic (not integer casts) keeps the global address space,
+   so these are global_load_dword, not flat loads. */
 FD_DEV uint32_t fd_ld_u32_unaligned( uint8_t const * p ) {
-  uintptr_t a = (uintptr_t)p;
-  uint32_t const * w = (uint32_t const *)(a & ~(uintptr_t)3);
-  uint32_t lo = w[0], hi = w[1];
-  uint32_t sh = (uint32_t)(a & 3u) * 8u;
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+  uint32_t mis = (uint32_t)((uintptr_t)p & 3u);
+  uint32_t const * w = (uint32_t const *)(p - mis);
+  return __builtin_amdgcn_alignbit( w[1], w[0], mis * 8u );
 }
 
 FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
-  uintptr_t a = (uintptr_t)p;
-  uint32_t const * w = (uint32_t const *)(a & ~(uintptr_t)3);
+  uint32_t mis = (uint32_t)((uintptr_t)p & 3u);
+  uint32_t const * w = (uint32_t const *)(p - mis);
   uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-  uint32_t sh = (uint32_t)(a & 3u) * 8u;
-  uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
-  uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
-  return ((uint64_t)hi << 32) | lo;
+  return ((uint64_t)__builtin_amdgcn_alignbit( w2, w1, mis * 8u ) << 32) | __builtin_amdgcn_alignbit( w1, w0, mis * 8u );
 }
 
+#define FD_SHA_ROUND(j,kt) do {                                                   \
+    uint64_t S1 = fd_rotr64(e,14) ^ fd_rotr64(e,18) ^ fd_rotr64(e,41);          \
+    uint64_t ch = (e&f) ^ (~e&g);                                               \
+    uint64_t t1 = h + S1 + ch + (kt) + w[j];                                    \
+    uint64_t S0 = fd_rotr64(a,28) ^ fd_rotr64(a,34) ^ fd_rotr64(a,39);          \
+    uint64_t mj = (a&b) ^ (a&c) ^ (b&c);                                        \
+    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;                           \
+  } while(0)
+
+/* 80 rounds as 16 + 4 x 16 so every index into the 16-word schedule
+   ring is a compile-time constant (no dynamic register indexing). */
 FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
   uint64_t a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
 #pragma unroll
-  for( int t=0; t<80; t++ ) {
-    if( t>=16 ) {
-      uint64_t w15 = w[(t-15)&15], w2 = w[(t-2)&15];
-      uint64_t s0 = fd_rotr64(w15,1) ^ fd_rotr64(w15,8) ^ (w15>>7);
-      uint64_t s1 = fd_rotr64(w2,19) ^ fd_rotr64(w2,61) ^ (w2>>6);
-      w[t&15] = w[t&15] + s0 + w[(t-7)&15] + s1;
+  for( int j=0; j<16; j++ ) FD_SHA_ROUND( j, fd_gpu_sha512_k[j] );
+#pragma unroll 1
+  for( int r=16; r<80; r+=16 ) {
+#pragma unroll
+    for( int j=0; j<16; j++ ) {
+      uint64_t w15 = w[(j+1)&15], w2 = w[(j+14)&15];
+      uint64_t s0 = fd_rotr64(w15,1) ^ fd_rotr64(w15,8) ^ fd_shr64(w15,7);
+      uint64_t s1 = fd_rotr64(w2,19) ^ fd_rotr64(w2,61) ^ fd_shr64(w2,6);
+      w[j] = w[j] + s0 + w[(j+9)&15] + s1;
+      FD_SHA_ROUND( j, fd_gpu_sha512_k[r+j] );
     }
-    uint64_t S1 = fd_rotr64(e,14) ^ fd_rotr64(e,18) ^ fd_rotr64(e,41);
-    uint64_t ch = (e&f) ^ (~e&g);
-    uint64_t t1 = h + S1 + ch + fd_gpu_sha512_k[t] + w[t&15];
-    uint64_t S0 = fd_rotr64(a,28) ^ fd_rotr64(a,34) ^ fd_rotr64(a,39);
-    uint64_t mj = (a&b) ^ (a&c) ^ (b&c);
-    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;
   }
   st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
 }
 
-/* SHA-512 of R(32) || A(32) || M(sz).  Words never straddle the R/A/M
-   boundaries (32 and 64 are multiples of 8).  Returns the digest as 8
-   little-endian-loaded 64-bit words (digest bytes 8i..8i+7 in word i,
-   byte 8i in the low byte). */
+/* SHA-512 of R(32) || A(32) || M(sz), one lane per message.  Each
+   128-byte message block is fetched as 33 aligned dwords and realigned
+   with v_alignbit (words never straddle the R/A/M boundaries: 32 and 64
+   are multiples of 8).  Returns the digest as 8 words where word i holds
+   digest bytes 8i..8i+7 little endian. */
 FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
   uint64_t st[8] = { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
                      0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL };
   uint64_t L = 64ULL + sz;                           /* bytes hashed */
   uint32_t nblk = (uint32_t)((L + 17ULL + 127ULL) >> 7);
+  uint32_t mis = (uint32_t)((uintptr_t)M & 3u);
+  uint32_t const * mw = (uint32_t const *)(M - mis);  /* aligned view of M */
+  uint32_t sh = mis * 8u;
   for( uint32_t b=0; b<nblk; b++ ) {
     uint64_t w[16];
+    if( b == 0 ) {
+#pragma unroll
+      for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
+#pragma unroll
+      for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
+    }
+    /* message dwords covering this block's message bytes */
+    int first = b == 0 ? 8 : 0;
+    int64_t mbase = (int64_t)b*128 - 64;             /* message offset of word 0 of this block */
 #pragma unroll
     for( int i=0; i<16; i++ ) {
-      uint64_t pos = ((uint64_t)b << 7) + 8u*(uint64_t)i;
-      uint64_t v;                                   /* bytes as loaded little endian */
-      if( pos < 32 )       v = fd_ld_u64_unaligned( R + pos );
-      else if( pos < 64 )  v = fd_ld_u64_unaligned( A + (pos-32) );
-      else {
-        uint64_t mp = pos - 64;
-        if( mp + 8 <= sz ) v = fd_ld_u64_unaligned( M + mp );
-        else {
-          v = 0;
-          if( mp < sz ) {
-            uint64_t keep = sz - mp;                 /* 1..7 bytes of message */
-            v = fd_ld_u64_unaligned( M + mp ) & ((1ULL << (8*keep)) - 1ULL);
-          }
-          if( pos <= L && L < pos + 8 ) v |= 0x80ULL << (8*(L-pos));
+      if( i < first ) continue;
+      int64_t mp = mbase + 8*i;                      /* message byte offset of this word */
+      uint64_t v = 0;
+      if( mp + 8 <= (int64_t)sz ) {
+        uint32_t const * q = mw + (mp >> 2);
+        uint32_t q0 = q[0], q1 = q[1], q2 = q[2];
+        v = ((uint64_t)__builtin_amdgcn_alignbit( q2, q1, sh ) << 32) | __builtin_amdgcn_alignbit( q1, q0, sh );
+      } else {
+        if( mp < (int64_t)sz ) {
+          uint64_t keep = (uint64_t)((int64_t)sz - mp);  /* 1..7 bytes */
+          uint32_t const * q = mw + (mp >> 2);
+          uint32_t q0 = q[0], q1 = q[1], q2 = q[2];
+          v = ((uint64_t)__builtin_amdgcn_alignbit( q2, q1, sh ) << 32) | __builtin_amdgcn_alignbit( q1, q0, sh );
+          v &= (1ULL << (8*keep)) - 1ULL;
         }
+        uint64_t pos = (uint64_t)(mp + 64);
+        if( pos <= L && L < pos + 8 ) v |= 0x80ULL << (8*(L-pos));
       }
       uint64_t be = fd_bswap64( v );
-      if( b==nblk-1 && i==15 ) be = L << 3;        /* bit count, low 64 bits */
-      /* bit count high word (i==14) is 0 for any 32-bit sz */
+      if( b==nblk-1 && i==15 ) be = L << 3;          /* bit count (high word 0) */
       w[i] = be;
     }
     fd_sha512_compress( st, w );
