@@ -390,17 +390,29 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
    multiples of -A in cached form) is kept in a per-signature SoA scratch
    table [8][4][10][n] in HBM (L2-resident while the launch runs). */
 
-FD_DEV void fd_tab_store( int32_t * tab, uint64_t n, uint64_t i, int e, fe4 const & v ) {
+/* Per-signature Ai table, AoS: tab[sig][entry][lane][limb] int32, one
+   160-byte entry per (sig, e).  An add step reads one whole entry of its
+   own signature as 10 x 16-byte loads; with the SoA layout each active
+   lane would touch 40 separate cache lines (measured 21 GB fetched per
+   262K-signature launch). */
+FD_DEV void fd_tab_store( int32_t * tab, uint64_t i, int e, fe4 const & v ) {
+  int4 * p = (int4 *)(tab + i*320 + (uint64_t)e*40);
 #pragma unroll
-  for( int l=0; l<4; l++ )
-#pragma unroll
-    for( int k=0; k<10; k++ ) tab[((uint64_t)(e*40 + l*10 + k))*n + i] = v.l[l].v[k];
+  for( int c=0; c<10; c++ ) {
+    int q = 4*c;
+    p[c] = make_int4( v.l[(q+0)/10].v[(q+0)%10], v.l[(q+1)/10].v[(q+1)%10],
+                      v.l[(q+2)/10].v[(q+2)%10], v.l[(q+3)/10].v[(q+3)%10] );
+  }
 }
-FD_DEV void fd_tab_load( fe4 & v, int32_t const * tab, uint64_t n, uint64_t i, int e ) {
+FD_DEV void fd_tab_load( fe4 & v, int32_t const * tab, uint64_t i, int e ) {
+  int4 const * p = (int4 const *)(tab + i*320 + (uint64_t)e*40);
 #pragma unroll
-  for( int l=0; l<4; l++ )
-#pragma unroll
-    for( int k=0; k<10; k++ ) v.l[l].v[k] = tab[((uint64_t)(e*40 + l*10 + k))*n + i];
+  for( int c=0; c<10; c++ ) {
+    int4 x = p[c];
+    int q = 4*c;
+    v.l[(q+0)/10].v[(q+0)%10] = x.x; v.l[(q+1)/10].v[(q+1)%10] = x.y;
+    v.l[(q+2)/10].v[(q+2)%10] = x.z; v.l[(q+3)/10].v[(q+3)%10] = x.w;
+  }
 }
 
 FD_DEV int fd_wave_min( int x ) {
@@ -457,7 +469,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
   d111.l[3] = FD_GPU_D2;
   v_mul( vu, vr, d111 ); v_subadd_12( vu );
-  fd_tab_store( tab, n, ii, 0, vu );
+  fd_tab_store( tab, ii, 0, vu );
   v_p2_dbl( vt, vr.l[2], vr.l[1], vr.l[0] );
   {
     fe4 a, b;   /* vr = MUL(perm(vt,3,2,3,1), perm(vt,2,1,0,0)) */
@@ -474,7 +486,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
     b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
     v_mul( vt, a, b );
     v_mul( vu, vt, d111 ); v_subadd_12( vu );
-    fd_tab_store( tab, n, ii, e+1, vu );
+    fd_tab_store( tab, ii, e+1, vu );
   }
 
   /* Main loop as a per-lane op stream (avx/fd_ed25519_ge.c:488-523
@@ -498,30 +510,29 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
     /* operands of the op's four multiplies, built lane by lane; the table
        entry is read lane by lane by add steps only (the Ai table does not
        fit the caches at full batch size, so D steps must not touch it) */
-    int tb = op & 0x40;
-    int32_t const * trow = tab + (uint64_t)(e*40)*n + ii;
+    fe4 ent;
+    if( op & 0x40 )  ent = fd_gpu_bi_precomp[e];
+    else if( is_add ) fd_tab_load( ent, tab, ii, e );
+    else {
+#pragma unroll
+      for( int l=0; l<4; l++ ) fd_fe_set( ent.l[l], 0 );
+    }
     fe4 h;
 #pragma unroll
     for( int l=0; l<4; l++ ) {
       /* entry lane: lanes 1,2 swapped for a negative digit */
-      int el = (l==1 || l==2) ? (neg ? 3-l : l) : l;
-      fe ent;
-      if( tb ) ent = fd_gpu_bi_precomp[e].l[el];
-      else if( is_add ) {
-#pragma unroll
-        for( int k=0; k<10; k++ ) ent.v[k] = trow[(uint64_t)(el*10 + k)*n];
-      } else fd_fe_set( ent, 0 );
       fe f, g;
 #pragma unroll
       for( int k=0; k<10; k++ ) {
         uint32_t z = q.l[0].v[k], y = q.l[1].v[k], x = q.l[2].v[k], t = q.l[3].v[k];
         uint32_t fa, fd, gd;
-        if( l==0 ) { fa = z;   fd = x+y; gd = x+y;  }
-        if( l==1 ) { fa = y-x; fd = y;   gd = y;    }
-        if( l==2 ) { fa = y+x; fd = x;   gd = x;    }
-        if( l==3 ) { fa = t;   fd = z;   gd = 2u*z; }
+        int32_t  ga;
+        if( l==0 ) { fa = z;   fd = x+y; gd = x+y;  ga = ent.l[0].v[k]; }
+        if( l==1 ) { fa = y-x; fd = y;   gd = y;    ga = neg ? ent.l[2].v[k] : ent.l[1].v[k]; }
+        if( l==2 ) { fa = y+x; fd = x;   gd = x;    ga = neg ? ent.l[1].v[k] : ent.l[2].v[k]; }
+        if( l==3 ) { fa = t;   fd = z;   gd = 2u*z; ga = ent.l[3].v[k]; }
         f.v[k] = (int32_t)(is_add ? fa : fd);
-        g.v[k] = is_add ? ent.v[k] : (int32_t)gd;
+        g.v[k] = is_add ? ga : (int32_t)gd;
       }
       fd_fe_mul( h.l[l], f, g );
     }

@@ -11,7 +11,7 @@
      op_start int32 [N]          first op index (FD_OPS_MAX if none)
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
-     tab      int32 [320][N]     per-signature Ai table (8 x 4 lanes x 10) */
+     tab      int32 [N][320]     per-signature Ai table (8 x 4 lanes x 10), AoS */
 typedef struct fd_ed25519_gpu_work {
   int32_t * status;
   uint8_t * ops;
