@@ -27,6 +27,12 @@
 typedef struct { int32_t v[10]; } fd_gpu_fe_t;
 typedef struct { fd_gpu_fe_t l[4]; } fd_gpu_fe4_t;
 
+/* Value barrier: hides what the compiler knows about x (e.g. that a
+   carried limb fits 26 bits).  Without it LLVM rewrites the signed
+   products of carried limbs into v_mad_u64_u32 + sign-fix sequences
+   (3-4 instructions per product instead of one v_mad_i64_i32). */
+FD_DEV int32_t fd_opaque( int32_t x ) { asm( "" : "+v"(x) ); return x; }
+
 FD_DEV int32_t fd_sext26( int64_t x ) { return ((int32_t)((uint32_t)x << 6)) >> 6; }
 FD_DEV int32_t fd_sext25( int64_t x ) { return ((int32_t)((uint32_t)x << 7)) >> 7; }
 
@@ -44,7 +50,7 @@ FD_DEV void fd_fe_carry( fd_gpu_fe_t & out, int64_t (&h)[10] ) {
   FD_C25X19( h[9], h[0] );
   FD_C26( h[0], h[1] );
 #pragma unroll
-  for( int i=0; i<10; i++ ) out.v[i] = (int32_t)h[i];
+  for( int i=0; i<10; i++ ) out.v[i] = fd_opaque( (int32_t)h[i] );
 }
 
 FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return c + (int64_t)a * (int64_t)b; }
@@ -55,8 +61,8 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
   int32_t f2[10], g19[10];
 #pragma unroll
   for( int i=0; i<10; i++ ) {
-    f2[i]  = (i&1) ? (int32_t)(2u*(uint32_t)f.v[i]) : f.v[i];
-    g19[i] = (int32_t)(19u*(uint32_t)g.v[i]);
+    f2[i]  = (i&1) ? fd_opaque( (int32_t)(2u*(uint32_t)f.v[i]) ) : f.v[i];
+    g19[i] = fd_opaque( (int32_t)(19u*(uint32_t)g.v[i]) );
   }
   int64_t s[10];
 #pragma unroll
@@ -80,9 +86,9 @@ FD_DEV void fd_fe_sqn( fd_gpu_fe_t & h, fd_gpu_fe_t const & fe, int n ) {
 #pragma unroll
   for( int i=0; i<10; i++ ) {
     F[i]   = fe.v[i];
-    F2[i]  = (int32_t)(2u *(uint32_t)fe.v[i]);
-    F19[i] = (int32_t)(19u*(uint32_t)fe.v[i]);
-    F38[i] = (int32_t)(38u*(uint32_t)fe.v[i]);
+    F2[i]  = fd_opaque( (int32_t)(2u *(uint32_t)fe.v[i]) );
+    F19[i] = fd_opaque( (int32_t)(19u*(uint32_t)fe.v[i]) );
+    F38[i] = fd_opaque( (int32_t)(38u*(uint32_t)fe.v[i]) );
   }
   int64_t s[10];
   s[0] = fd_mad(F[0],F[0],0);  s[0]=fd_mad(F2[1],F38[9],s[0]); s[0]=fd_mad(F2[2],F19[8],s[0]); s[0]=fd_mad(F2[3],F38[7],s[0]); s[0]=fd_mad(F2[4],F19[6],s[0]); s[0]=fd_mad(F[5],F38[5],s[0]);
