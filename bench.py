@@ -39,12 +39,38 @@ BATCH_SIGS = 4096
 STEP_BATCHES = 64
 UNIQUE_SIGS = 65536
 
-# ---- algorithmic work model ----
-OPS_PER_FIELD_MUL = 490          # 10x10 schoolbook + carry chain, int32 ops
-OPS_PER_SHA_BLOCK = 4900         # 80 rounds + schedule, as 32-bit-pair ops
-FMUL_DSM = 2538                  # Ai table 96 + 251.5 dbl x 7 + 84.9 add x 8 + compare 2
-FMUL_DECOMP = 606                # 2 points x (pow22523 265 + 12 + small-order 26)
-PEAK_INT32_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 T/s
+# ---- algorithmic work model --------------------------
+# The path is bound by integer VALU issue.  Work is counted as the REFERENCE
+# algorithm's operations (its field multiplies and squarings, SHA-512 blocks)
+# priced at their minimal gfx950 issue cost in full-rate int32 lane-op slots:
+#   a 32x32->64 multiply-accumulate (v_mad_i64_i32) issues at half rate = 2
+#   slots (profiles/ubench_int_r01.txt: 0.43-0.45 of the v_add_u32 rate),
+#   a 64-bit add/shift = 2 slots, a 32-bit op = 1 slot.
+# fe_mul (FE_AVX_INL_MUL, avx/fd_ed25519_fe_avx_inl.h:484-590): 100 MACs
+#   (200) + 15 operand pre-scales + 12 carries x (round 2 + shift 2 + add 2 +
+#   sext 1) = 299.  fe_sq (FE_AVX_INL_SQN, :592-677): 55 MACs (110) + 30
+#   pre-scales + 84 = 224; sq2 doubles 10 column sums (+20) = 244.
+# SHA-512 block: 80 rounds x 40 + 64-word schedule x 26 + 16 = 4,900
+#   (64-bit ops as 32-bit pairs).
+SLOT_MUL, SLOT_SQ, SLOT_SQ2 = 299, 224, 244
+SLOT_SHA_BLOCK = 4900
+# per-verify reference op counts (251.5 doublings and
+# 84.9 additions per verify, measured on the reference's slide statistics)
+N_DBL, N_ADD = 251.5, 84.9
+# fd_k_dsm: Ai table (avx/fd_ed25519_ge.c:423-481: 92 mul, 3 sq, 1 sq2);
+#   each doubling SQN(1,1,1,2) + one 4-lane conversion MUL; each addition
+#   one 4-lane MUL + conversion MUL; compare 2 mul (fd_ed25519_user.c:419-427);
+#   lane mixes DBL_MIX+X+Y 50, SUBADD_12+SUB_MIX 70 int32 ops.
+SLOTS_DSM = ((92 + 4 * N_DBL + 8 * N_ADD + 2) * SLOT_MUL + (3 + 3 * N_DBL) * SLOT_SQ
+             + (1 + N_DBL) * SLOT_SQ2 + 50 * N_DBL + 70 * N_ADD)
+# fd_k_decomp, per point (avx/fd_ed25519_ge.c:222-299 + fd_ed25519_ge.c:11-66):
+#   264 sq + 3 sq2 (pow22523 251, 4 around it, small-order 3 x 4) and 32 mul,
+#   + frombytes 60 + 3 canonical reductions x 40; two points per verify.
+SLOTS_DECOMP = 2 * (264 * SLOT_SQ + 3 * SLOT_SQ2 + 32 * SLOT_MUL + 60 + 120)
+# fd_k_prep: SHA-512 blocks + S check, sc_reduce (~600) and two wNAF-5
+#   recodings (~1,700 each) = 4,000 fixed.
+SLOTS_PREP_FIXED = 4000
+PEAK_INT32_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T slots/s
 
 
 def sha_blocks(msg_sz):
@@ -61,7 +87,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=300)
-    ap.add_argument("--cpu-sample", type=int, default=196608, help="signatures in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -196,9 +222,9 @@ def main():
         ks /= reps
         msz = base.desc["msg_sz"].astype(np.int64)
         blocks = float(np.mean([sha_blocks(int(m)) for m in msz]))
-        ops = {"fd_k_prep": OPS_PER_SHA_BLOCK * blocks * n_step,
-               "fd_k_decomp": FMUL_DECOMP * OPS_PER_FIELD_MUL * n_step,
-               "fd_k_dsm": FMUL_DSM * OPS_PER_FIELD_MUL * n_step}
+        ops = {"fd_k_prep": (SLOT_SHA_BLOCK * blocks + SLOTS_PREP_FIXED) * n_step,
+               "fd_k_decomp": SLOTS_DECOMP * n_step,
+               "fd_k_dsm": SLOTS_DSM * n_step}
         kern = {}
         for name, ms in zip(fa.Engine.KERNELS, ks):
             ach = ops[name] / (ms * 1e-3) / 1e12
@@ -212,7 +238,7 @@ def main():
                     traffic = tr.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        w_total = (FMUL_DSM + FMUL_DECOMP) * OPS_PER_FIELD_MUL + OPS_PER_SHA_BLOCK * blocks
+        w_total = SLOTS_DSM + SLOTS_DECOMP + SLOT_SHA_BLOCK * blocks + SLOTS_PREP_FIXED
         res["roofline"] = {
             "bound": "valu-int32",
             "kernel": dom,
@@ -224,6 +250,12 @@ def main():
             "per_kernel": kern,
             "pipeline_frac": value * w_total / PEAK_INT32_OPS,
             "ops_per_verify": w_total,
+            "work_model": "reference field-op / SHA-block counts x minimal gfx950 issue slots "
+                          "(MAC and 64-bit ops 2, int32 op 1); peak = 78.6 T full-rate int32 lane-op "
+                          "slots/s (DESIGN.md section 4)",
+            "traffic_note": "HBM bytes per launch of the dominant kernel from rocprofv3 PMC "
+                            "(2*FETCH_SIZE + WRITE_SIZE, profiles/pmc_traffic.json); the path is "
+                            "VALU-bound, traffic is a secondary check",
         }
         if not a.no_latency:
             res["latency"] = latency(eng, base, a.latency_batches)
