@@ -99,6 +99,36 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_sign.restype = vp
         L.fd_ed25519_sign_batch.argtypes = [ul, vp, vp, vp, vp, vp, vp, ip]
         L.fd_ed25519_sign_batch.restype = None
+        L.fd_ed25519_gpu_new_ex.argtypes = [ip, ul, ul, ip]
+        L.fd_ed25519_gpu_new_ex.restype = vp
+        L.fd_ed25519_gpu_max_sigs.argtypes = [vp]
+        L.fd_ed25519_gpu_max_sigs.restype = ul
+        L.fd_ed25519_gpu_max_blob.argtypes = [vp]
+        L.fd_ed25519_gpu_max_blob.restype = ul
+        L.fd_ed25519_gpu_stage.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.fd_ed25519_gpu_stage.restype = ip
+        L.fd_ed25519_gpu_unstage.argtypes = [vp, vp]
+        L.fd_ed25519_gpu_unstage.restype = None
+        L.fd_txn_parse.argtypes = [vp, ul, vp, vp]
+        L.fd_txn_parse.restype = ul
+        L.fd_verify_tile_new.argtypes = [vp, vp, vp, vp]
+        L.fd_verify_tile_new.restype = vp
+        L.fd_verify_tile_delete.argtypes = [vp]
+        L.fd_verify_tile_delete.restype = None
+        L.fd_verify_tile_rx.argtypes = [vp, vp, ul, ul, ul]
+        L.fd_verify_tile_rx.restype = ip
+        L.fd_verify_tile_rx_burst.argtypes = [vp, vp, vp, vp, vp, vp, ul]
+        L.fd_verify_tile_rx_burst.restype = ip
+        L.fd_verify_tile_service.argtypes = [vp, ip]
+        L.fd_verify_tile_service.restype = ip
+        L.fd_verify_tile_diag.argtypes = [vp, vp]
+        L.fd_verify_tile_diag.restype = None
+        L.fd_vt_tcache_new.argtypes = [ul, ul]
+        L.fd_vt_tcache_new.restype = vp
+        L.fd_vt_tcache_insert.argtypes = [vp, ul]
+        L.fd_vt_tcache_insert.restype = ip
+        L.fd_vt_tcache_delete.argtypes = [vp]
+        L.fd_vt_tcache_delete.restype = None
         _lib = L
     return _lib
 
@@ -118,9 +148,9 @@ def last_error() -> str:
 class Engine:
     """One verification engine bound to one gfx950 device (fd_ed25519_gpu_t)."""
 
-    def __init__(self, device: int = 0, max_sigs: int = 1 << 16, max_blob: int = 1 << 26):
+    def __init__(self, device: int = 0, max_sigs: int = 1 << 16, max_blob: int = 1 << 26, depth: int = 3):
         L = lib()
-        self._h = L.fd_ed25519_gpu_new(device, max_sigs, max_blob)
+        self._h = L.fd_ed25519_gpu_new_ex(device, max_sigs, max_blob, depth)
         if not self._h:
             raise EngineError(f"fd_ed25519_gpu_new(device={device}) failed: {last_error()}")
         self.device = device

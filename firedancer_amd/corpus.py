@@ -200,9 +200,9 @@ def solana_txns(n_sigs, seed=0, p2=0.3, max_sigs_per_txn=2, nthreads=8, sig_dist
     """C2/C5: legacy Solana txns of exactly TXN_MTU bytes.
 
     payload = compact_u16(k) | k x sig | message, message =
-      header(3) | compact_u16(m) | m x 32-byte account keys (signers first) |
+      header(3) | compact_u16(k+1) | k signer keys + 1 program key |
       blockhash(32) | compact_u16(1) | one instruction whose data fills the
-      MTU.  Every txn parses with firedancer_amd.txn.parse.
+      MTU (up to 12 signatures fit).  Every txn parses with fd_txn_parse.
     Signature j covers message = payload[1+64k:] with account key j.
     sig count: 1 or 2 with p(2)=p2, or drawn from sig_dist (list of
     probabilities for k = 1..len)."""
@@ -229,7 +229,7 @@ def solana_txns(n_sigs, seed=0, p2=0.3, max_sigs_per_txn=2, nthreads=8, sig_dist
     filler = rng.integers(0, 256, TXN_MTU, dtype=np.uint8)
     for t, k in enumerate(ks):
         b = t * TXN_MTU
-        m = k + 2  # signers + 2 program/readonly accounts
+        m = k + 1  # signers + the (readonly, unsigned) program account
         mo = b + 1 + 64 * k
         blob[b] = k
         blob[mo:mo + 3] = (k, 0, 1)
@@ -238,17 +238,23 @@ def solana_txns(n_sigs, seed=0, p2=0.3, max_sigs_per_txn=2, nthreads=8, sig_dist
             blob[mo + 4 + 32 * j: mo + 4 + 32 * (j + 1)] = pubs[s + j]
         rest = mo + 4 + 32 * m                  # after the account keys
         blob[mo + 4 + 32 * k:rest] = filler[:32 * (m - k)]
-        blob[rest:rest + 32] = filler[32:64]    # recent blockhash
+        blob[rest:rest + 32] = filler[32:64]    # recent blockhash, unique per txn
+        blob[rest:rest + 8] = np.frombuffer(np.uint64(t).tobytes(), np.uint8)
+        blob[rest + 8:rest + 16] = np.frombuffer(np.uint64(seed).tobytes(), np.uint8)
         rest += 32
-        dl = b + TXN_MTU - (rest + 1 + 1 + 1 + 2)
+        room = b + TXN_MTU - (rest + 3)         # instr count, program id, account count
+        dl = room - 1 if room - 1 < 128 else room - 2
         blob[rest] = 1                          # one instruction
         blob[rest + 1] = m - 1                  # program id index
         blob[rest + 2] = 0                      # no account indices
-        blob[rest + 3] = 0x80 | (dl & 0x7F)     # compact-u16 data length
-        blob[rest + 4] = dl >> 7
-        blob[rest + 5:b + TXN_MTU] = filler[:dl]
-        # unique per txn so no two messages collide
-        blob[rest + 5:rest + 13] = np.frombuffer(np.uint64(t).tobytes(), np.uint8)
+        if dl < 128:                            # minimal compact-u16 data length
+            blob[rest + 3] = dl
+            d0 = rest + 4
+        else:
+            blob[rest + 3] = 0x80 | (dl & 0x7F)
+            blob[rest + 4] = dl >> 7
+            d0 = rest + 5
+        blob[d0:b + TXN_MTU] = filler[:dl]
         for j in range(k):
             desc[s + j] = (b + 1 + 64 * j, mo + 4 + 32 * j, mo, TXN_MTU - 1 - 64 * k)
             msg_off[s + j] = mo

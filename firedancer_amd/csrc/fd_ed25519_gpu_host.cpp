@@ -4,7 +4,7 @@
    One engine per device.  The engine owns:
      - device buffers for one batch of capacity (max_sigs, max_blob) per
        ring slot: blob, descriptors, result codes and the HBM working set;
-     - FD_GPU_DEPTH pinned host slots (blob, desc, out) and one HIP stream
+     - depth (default 3, up to 8) pinned host slots (blob, desc, out) and one HIP stream
        per slot, so batch b+1's H2D copy overlaps batch b's kernels and
        batch b-1's D2H copy (double/triple buffering);
    All allocation happens in fd_ed25519_gpu_new (the verify tile calls it
@@ -21,7 +21,8 @@
 #include <atomic>
 #include "fd_ed25519_gpu_private.h"
 
-#define FD_GPU_DEPTH 3
+#define FD_GPU_DEPTH_DEFAULT 3
+#define FD_GPU_DEPTH_MAX     8
 #define FD_BLOB_PAD  64UL
 
 struct fd_ed25519_gpu_slot {
@@ -39,6 +40,7 @@ struct fd_ed25519_gpu_slot {
   hipEvent_t              done;
   unsigned long           n;
   unsigned long           ticket;   /* 0 = free */
+  int                     staged;   /* pinned buffers lent out by fd_ed25519_gpu_stage */
 };
 
 struct fd_ed25519_gpu {
@@ -46,7 +48,8 @@ struct fd_ed25519_gpu {
   unsigned long max_sigs;
   unsigned long max_blob;
   unsigned long next_ticket;
-  fd_ed25519_gpu_slot slot[FD_GPU_DEPTH];
+  int           depth;
+  fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
 };
@@ -85,7 +88,11 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
 }
 
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob ) {
-  if( !max_sigs || max_sigs > (1UL<<28) || max_blob > (1UL<<32) - FD_BLOB_PAD ) {
+  return fd_ed25519_gpu_new_ex( device, max_sigs, max_blob, FD_GPU_DEPTH_DEFAULT );
+}
+
+extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long max_sigs, unsigned long max_blob, int depth ) {
+  if( !max_sigs || max_sigs > (1UL<<28) || max_blob > (1UL<<32) - FD_BLOB_PAD || depth < 1 || depth > FD_GPU_DEPTH_MAX ) {
     snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_new: bad capacity" );
     return NULL;
   }
@@ -100,11 +107,11 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_
     return NULL;
   }
   fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
-  g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1;
+  g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   unsigned long blob_cap = max_blob + FD_BLOB_PAD;
   HIPCHK( hipSetDevice( device ) );
   HIPCHK( fd_ed25519_gpu_upload_tables() );
-  for( int s=0; s<FD_GPU_DEPTH; s++ ) {
+  for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     HIPCHK( hipHostMalloc( (void **)&sl->h_blob, blob_cap, hipHostMallocDefault ) );
     HIPCHK( hipHostMalloc( (void **)&sl->h_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t), hipHostMallocDefault ) );
@@ -129,7 +136,7 @@ fail:
 extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   if( !g ) return;
   hipSetDevice( g->device );
-  for( int s=0; s<FD_GPU_DEPTH; s++ ) {
+  for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( sl->stream ) hipStreamSynchronize( sl->stream );
     if( sl->h_blob ) hipHostFree( sl->h_blob );
@@ -146,7 +153,33 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   delete g;
 }
 
-extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { (void)g; return FD_GPU_DEPTH; }
+extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
+extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
+extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
+
+/* Lend a free slot's pinned staging buffers (zero-copy submit). */
+extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
+  if( !g || !blob || !desc ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int s=0; s<g->depth; s++ ) {
+    fd_ed25519_gpu_slot * sl = &g->slot[s];
+    if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->h_blob; *desc = sl->h_desc; return 0; }
+  }
+  return FD_ED25519_ERR_ARG;
+}
+
+extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
+  if( !g ) return;
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) g->slot[s].staged = 0;
+}
+
+/* a free slot: the staged one owning `blob` if any, else any unstaged one */
+static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * blob ) {
+  for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && g->slot[s].h_blob == blob ) return &g->slot[s];
+  for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) return &g->slot[s];
+  return NULL;
+}
 extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? g->device : -1; }
 
 /* Bounds check one descriptor against the blob (the reference does no
@@ -231,9 +264,8 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   /* use a free slot; synchronous callers serialise on the lock */
-  fd_ed25519_gpu_slot * sl = NULL;
-  for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( !g->slot[s].ticket ) sl = &g->slot[s];
-  if( !sl ) { sl = &g->slot[0]; hipEventSynchronize( sl->done ); }
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
+  if( !sl ) return FD_ED25519_ERR_ARG;   /* every slot in flight or lent out */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
   if( (e = hipEventSynchronize( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
@@ -247,11 +279,11 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  fd_ed25519_gpu_slot * sl = NULL;
-  for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( !g->slot[s].ticket ) sl = &g->slot[s];
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
   if( !sl ) return FD_ED25519_ERR_ARG;   /* ring full: poll first */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
+  sl->staged = 0;
   /* keep what collect needs for the bounds report */
   sl->ticket = g->next_ticket++;
   *ticket = sl->ticket;
@@ -263,7 +295,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   fd_ed25519_gpu_slot * sl = NULL;
   {
     std::lock_guard<std::mutex> guard( g->lock );
-    for( int s=0; s<FD_GPU_DEPTH && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
+    for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
   hipError_t e = block ? hipEventSynchronize( sl->done ) : hipEventQuery( sl->done );
@@ -303,8 +335,8 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  fd_ed25519_gpu_slot * sl = &g->slot[0];
-  hipEventSynchronize( sl->done );
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
+  if( !sl ) return FD_ED25519_ERR_ARG;
   unsigned long i = 0;
   while( i < n ) {
     /* fill one chunk */

@@ -1,0 +1,306 @@
+/* fd_verify_tile.cpp -- the verify tile's HA dedup + batched GPU
+   signature verification + in-order publish (include/fd_verify_tile.h;
+   reference behaviour: src/app/frank/load/fd_frank_verify_synth_load.c:
+   360-410, frag format src/disco/quic/fd_quic_tile.c:475-516).
+
+   Data flow per frag (host, single thread, as the reference tile):
+     trailer -> fd_txn_t (signature / signer / message offsets)
+     tag = first 8 bytes of signature 0 -> tcache; dup -> HA_FILT
+     frag bytes -> the open batch's pinned staging blob (zero-copy submit:
+       the blob IS the engine ring slot's pinned buffer), one descriptor
+       per signature pointing into it
+     batch full -> fd_ed25519_gpu_submit (H2D, 3 kernels, D2H on the slot's
+       stream); the tile keeps filling the next slot meanwhile
+     completed batches, oldest first -> publish txns whose signatures all
+       verified, SV_FILT the rest */
+
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <deque>
+#include <vector>
+#include "fd_verify_tile.h"
+#include "fd_txn_abi.h"
+
+#define FD_EXPORT extern "C" __attribute__((visibility("default")))
+
+/* ---- HA dedup: last `depth` distinct tags ------------------------------ */
+
+struct fd_vt_tcache {
+  unsigned long   depth, map_cnt, oldest, shift;
+  unsigned long * ring;   /* depth tags, 0 = empty */
+  unsigned long * map;    /* open addressing, linear probing, 0 = empty */
+};
+
+static inline unsigned long fd_vt_slot0( fd_vt_tcache_t const * tc, unsigned long tag ) {
+  return (tag * 0x9e3779b97f4a7c15UL) >> tc->shift;
+}
+
+/* index of tag in the map, or of the empty slot where it would go */
+static unsigned long fd_vt_find( fd_vt_tcache_t const * tc, unsigned long tag, int * found ) {
+  unsigned long m = tc->map_cnt - 1UL, i = fd_vt_slot0( tc, tag );
+  for(;;) {
+    unsigned long t = tc->map[ i ];
+    if( t == tag ) { *found = 1; return i; }
+    if( !t )       { *found = 0; return i; }
+    i = (i + 1UL) & m;
+  }
+}
+
+static void fd_vt_erase( fd_vt_tcache_t * tc, unsigned long tag ) {
+  if( !tag ) return;
+  int found; unsigned long hole = fd_vt_find( tc, tag, &found );
+  if( !found ) return;
+  unsigned long m = tc->map_cnt - 1UL, i = hole;
+  tc->map[ hole ] = 0UL;
+  /* backward-shift: pull later members of the probe run into the hole
+     when the hole lies on their probe path */
+  for(;;) {
+    i = (i + 1UL) & m;
+    unsigned long t = tc->map[ i ];
+    if( !t ) return;
+    unsigned long home = fd_vt_slot0( tc, t );
+    unsigned long d_hole = (hole - home) & m, d_i = (i - home) & m;
+    if( d_hole < d_i ) { tc->map[ hole ] = t; tc->map[ i ] = 0UL; hole = i; }
+  }
+}
+
+FD_EXPORT fd_vt_tcache_t * fd_vt_tcache_new( unsigned long depth, unsigned long map_cnt ) {
+  if( !depth || map_cnt < depth + 2UL || (map_cnt & (map_cnt - 1UL)) || map_cnt > (1UL << 40) ) return NULL;
+  fd_vt_tcache_t * tc = (fd_vt_tcache_t *)calloc( 1, sizeof(fd_vt_tcache_t) );
+  if( !tc ) return NULL;
+  tc->depth = depth; tc->map_cnt = map_cnt;
+  tc->shift = 64UL - (unsigned long)__builtin_ctzl( map_cnt );
+  if( map_cnt == 1UL ) tc->shift = 63UL;
+  tc->ring = (unsigned long *)calloc( depth, sizeof(unsigned long) );
+  tc->map  = (unsigned long *)calloc( map_cnt, sizeof(unsigned long) );
+  if( !tc->ring || !tc->map ) { free( tc->ring ); free( tc->map ); free( tc ); return NULL; }
+  return tc;
+}
+
+FD_EXPORT void fd_vt_tcache_delete( fd_vt_tcache_t * tc ) {
+  if( !tc ) return;
+  free( tc->ring ); free( tc->map ); free( tc );
+}
+
+FD_EXPORT int fd_vt_tcache_insert( fd_vt_tcache_t * tc, unsigned long tag ) {
+  if( !tag ) return 1;                       /* FD_TCACHE_TAG_NULL always matches */
+  int found; unsigned long at = fd_vt_find( tc, tag, &found );
+  if( found ) return 1;
+  tc->map[ at ] = tag;
+  unsigned long old = tc->ring[ tc->oldest ];
+  tc->ring[ tc->oldest ] = tag;
+  tc->oldest = tc->oldest + 1UL == tc->depth ? 0UL : tc->oldest + 1UL;
+  fd_vt_erase( tc, old );
+  return 0;
+}
+
+/* ---- the tile ------------------------------------------------------------ */
+
+struct fd_vt_txn {
+  uint64_t blob_off, sz, ctl, tsorig, tag;
+  uint32_t sig0, nsig;
+};
+
+struct fd_vt_batch {
+  uint8_t *               blob;   /* engine slot's pinned staging buffers */
+  fd_ed25519_gpu_desc_t * desc;
+  unsigned long           used, nsig, ticket;
+  std::vector<fd_vt_txn>  txns;
+};
+
+struct fd_verify_tile {
+  fd_ed25519_gpu_t *        gpu;
+  fd_verify_tile_publish_fn publish;
+  void *                    ctx;
+  fd_vt_tcache_t *          tc;
+  unsigned long             batch_sigs, max_blob;
+  fd_vt_batch *             open;        /* NULL until a slot is staged */
+  std::deque<fd_vt_batch *> inflight;    /* submitted, oldest first     */
+  std::vector<fd_vt_batch *> pool;
+  std::vector<int>          out;
+  unsigned long             diag[ FD_VERIFY_TILE_DIAG_CNT ];
+};
+
+static unsigned long fd_vt_now( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (unsigned long)ts.tv_sec * 1000000000UL + (unsigned long)ts.tv_nsec;
+}
+
+static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
+  int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), block );
+  if( r <= 0 ) return r ? FD_ED25519_ERR_GPU : 0;
+  unsigned long tspub = fd_vt_now();
+  for( fd_vt_txn const & x : b->txns ) {
+    int ok = 1;
+    for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( t->out[ x.sig0 + k ] == FD_ED25519_SUCCESS );
+    if( ok ) {
+      if( t->publish ) t->publish( t->ctx, x.tag, b->blob + x.blob_off, x.sz, x.ctl, x.tsorig, tspub );
+      t->diag[ FD_VERIFY_TILE_DIAG_PUB_CNT ]++;
+      t->diag[ FD_VERIFY_TILE_DIAG_PUB_SZ  ] += x.sz;
+    } else {
+      t->diag[ FD_VERIFY_TILE_DIAG_SV_FILT_CNT ]++;
+      t->diag[ FD_VERIFY_TILE_DIAG_SV_FILT_SZ  ] += x.sz;
+    }
+  }
+  b->txns.clear(); b->ticket = 0;
+  t->pool.push_back( b );
+  return 1;
+}
+
+/* publish finished batches in order; with block, at least the oldest */
+static int fd_vt_drain( fd_verify_tile_t * t, int block ) {
+  while( !t->inflight.empty() ) {
+    int r = fd_vt_complete( t, t->inflight.front(), block );
+    if( r < 0 ) return r;
+    if( !r ) break;
+    t->inflight.pop_front();
+    block = 0;
+  }
+  return 0;
+}
+
+static int fd_vt_submit( fd_verify_tile_t * t ) {
+  fd_vt_batch * b = t->open;
+  if( !b || !b->nsig ) return 0;
+  int err = fd_ed25519_gpu_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+  if( err ) return FD_ED25519_ERR_GPU;
+  t->diag[ FD_VERIFY_TILE_DIAG_BATCH_CNT ]++;
+  t->inflight.push_back( b );
+  t->open = NULL;
+  return 0;
+}
+
+/* make sure an open batch with room for nsig signatures / sz bytes exists */
+static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned long sz ) {
+  if( t->open && ( t->open->nsig + nsig > t->batch_sigs || t->open->used + sz > t->max_blob ) ) {
+    int err = fd_vt_submit( t );
+    if( err ) return err;
+  }
+  while( !t->open ) {
+    void * blob; fd_ed25519_gpu_desc_t * desc;
+    if( !fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ) {
+      fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
+      b->blob = (uint8_t *)blob; b->desc = desc; b->used = 0; b->nsig = 0; b->ticket = 0;
+      t->open = b;
+      break;
+    }
+    /* every ring slot busy: back-pressure until the oldest batch lands */
+    if( t->inflight.empty() ) return FD_ED25519_ERR_GPU;
+    t->diag[ FD_VERIFY_TILE_DIAG_BACKP_CNT ]++;
+    int err = fd_vt_drain( t, 1 );
+    if( err ) return err;
+  }
+  return 0;
+}
+
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
+                                                 fd_verify_tile_publish_fn publish, void * ctx ) {
+  if( !gpu ) return NULL;
+  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL };
+  if( cfg ) c = *cfg;
+  unsigned long maxs = fd_ed25519_gpu_max_sigs( gpu );
+  if( !c.batch_sigs || c.batch_sigs > maxs ) c.batch_sigs = maxs;
+  if( c.batch_sigs < FD_TXN_SIG_MAX ) return NULL;   /* a batch must hold the largest txn */
+  fd_vt_tcache_t * tc = fd_vt_tcache_new( c.tcache_depth, c.tcache_map_cnt );
+  if( !tc ) return NULL;
+  fd_verify_tile_t * t = new fd_verify_tile_t();
+  t->gpu = gpu; t->publish = publish; t->ctx = ctx; t->tc = tc;
+  t->batch_sigs = c.batch_sigs;
+  t->max_blob = fd_ed25519_gpu_max_blob( gpu );
+  t->open = NULL;
+  int depth = fd_ed25519_gpu_depth( gpu );
+  for( int i=0; i<depth; i++ ) { fd_vt_batch * b = new fd_vt_batch(); b->ticket = 0; t->pool.push_back( b ); }
+  t->out.resize( maxs );
+  memset( t->diag, 0, sizeof(t->diag) );
+  return t;
+}
+
+FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
+  if( !t ) return;
+  while( !t->inflight.empty() ) {   /* results discarded, but the slots must drain */
+    fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
+    fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
+    delete b;
+  }
+  if( t->open ) { fd_ed25519_gpu_unstage( t->gpu, t->open->blob ); delete t->open; }
+  for( fd_vt_batch * b : t->pool ) delete b;
+  fd_vt_tcache_delete( t->tc );
+  delete t;
+}
+
+FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
+                                 unsigned long tsorig ) {
+  uint8_t const * f = (uint8_t const *)frag;
+  /* trailer: [payload | pad to 2 | fd_txn_t | u16 payload_sz] */
+  if( !f || sz < 2UL + sizeof(fd_txn_t) ) goto bad;
+  {
+    unsigned long psz = (unsigned long)f[ sz-2 ] | ((unsigned long)f[ sz-1 ] << 8);
+    unsigned long toff = (psz + 1UL) & ~1UL;
+    if( psz > FD_TXN_MTU || toff + sizeof(fd_txn_t) + 2UL > sz ) goto bad;
+    fd_txn_t hdr;
+    memcpy( &hdr, f + toff, sizeof(fd_txn_t) );
+    unsigned long nsig = hdr.signature_cnt;
+    if( !nsig || nsig > FD_TXN_SIG_MAX || hdr.acct_addr_cnt < nsig
+        || (unsigned long)hdr.signature_off + 64UL*nsig > psz
+        || (unsigned long)hdr.acct_addr_off + 32UL*nsig > psz
+        || hdr.message_off > psz ) goto bad;
+
+    unsigned long tag;
+    memcpy( &tag, f + hdr.signature_off, 8 );
+    if( fd_vt_tcache_insert( t->tc, tag ) ) {
+      t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;
+      t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_SZ  ] += sz;
+      return 0;
+    }
+    unsigned long room = (sz + 7UL) & ~7UL;
+    if( room > t->max_blob ) goto bad;
+    int err = fd_vt_reserve( t, nsig, room );
+    if( err ) return err;
+    fd_vt_batch * b = t->open;
+    unsigned long base = b->used;
+    memcpy( b->blob + base, f, sz );
+    for( unsigned long k=0; k<nsig; k++ ) {
+      fd_ed25519_gpu_desc_t * d = &b->desc[ b->nsig + k ];
+      d->sig_off = (uint32_t)(base + hdr.signature_off + 64UL*k);
+      d->pub_off = (uint32_t)(base + hdr.acct_addr_off + 32UL*k);
+      d->msg_off = (uint32_t)(base + hdr.message_off);
+      d->msg_sz  = (uint32_t)(psz - hdr.message_off);
+    }
+    fd_vt_txn x = { base, sz, ctl, tsorig, tag, (uint32_t)b->nsig, (uint32_t)nsig };
+    b->txns.push_back( x );
+    b->nsig += nsig;
+    b->used += room;
+    t->diag[ FD_VERIFY_TILE_DIAG_SIG_CNT ] += nsig;
+    if( b->nsig == t->batch_sigs ) return fd_vt_submit( t );
+    return 0;
+  }
+bad:
+  t->diag[ FD_VERIFY_TILE_DIAG_BAD_CNT ]++;
+  return 0;
+}
+
+FD_EXPORT int fd_verify_tile_rx_burst( fd_verify_tile_t * t, uint8_t const * base, uint64_t const * off,
+                                       uint32_t const * sz, uint64_t const * ctl, uint64_t const * tsorig,
+                                       unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    int err = fd_verify_tile_rx( t, base + off[i], sz[i], ctl ? ctl[i] : 0UL, tsorig ? tsorig[i] : 0UL );
+    if( err ) return err;
+  }
+  return 0;
+}
+
+FD_EXPORT int fd_verify_tile_service( fd_verify_tile_t * t, int flush ) {
+  if( flush ) {
+    int err = fd_vt_submit( t );
+    if( err ) return err;
+    while( !t->inflight.empty() ) if( (err = fd_vt_drain( t, 1 )) ) return err;
+    return 0;
+  }
+  return fd_vt_drain( t, 0 );
+}
+
+FD_EXPORT void fd_verify_tile_diag( fd_verify_tile_t const * t, unsigned long * diag ) {
+  memcpy( diag, t->diag, sizeof(t->diag) );
+  diag[ FD_VERIFY_TILE_DIAG_IN_BACKP ] = 0UL;
+}

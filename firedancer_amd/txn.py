@@ -1,115 +1,75 @@
-"""Minimal Solana transaction wire parsing for the sigverify path.
+"""Solana transaction wire format for the sigverify path.
 
-Mirrors the parts of fd_txn_parse (src/ballet/txn/fd_txn_parse.c, layout
-in src/ballet/txn/fd_txn.h:159-217) that the verify tile needs: the
-signature count, the offsets of the signatures, of the signer account
-addresses and of the message.  Each transaction yields signature_cnt
-(sig_i, pub_i, msg) tuples with sig_i = payload[sig_off + 64 i],
-pub_i = payload[acct_off + 32 i], msg = payload[msg_off:]
-(src/wiredancer/test/test_wiredancer_demo.c:364-370).  Malformed input
-returns None (the reference drops such txns before verify).
+Thin ctypes layer over the native parser in libfd_ed25519_gpu.so
+(firedancer_amd/csrc/fd_txn_host.c, ABI include/fd_txn_abi.h), which
+restates src/ballet/txn/fd_txn_parse.c:7-217 and writes the reference's
+fd_txn_t byte layout (src/ballet/txn/fd_txn.h:107-320).
+
+  parse(payload)      -> dict of fd_txn_t fields (+ 'instr', 'luts', 'footprint',
+                         'raw' descriptor bytes) or None if malformed
+  descs_for(payload)  -> one engine descriptor per signature: signature i over
+                         the message with signer account i
+                         (src/ballet/txn/fd_txn.h:159-217)
+  frag(payload)       -> the QUIC tile's frag: payload | pad to 2 | fd_txn_t |
+                         u16 payload_sz (src/disco/quic/fd_quic_tile.c:475-516)
 """
 from __future__ import annotations
 
+import ctypes
+import struct
+
 import numpy as np
 
-from . import DESC_DTYPE
+from . import DESC_DTYPE, lib
 
-TXN_MTU = 1232
-SIG_MAX = 12  # FD_TXN_SIG_MAX, src/ballet/txn/fd_txn.h:55-57
-ACCT_ADDR_MAX = 128
+TXN_MTU = 1232            # FD_TPU_MTU
+SIG_MAX = 127             # FD_TXN_SIG_MAX, src/ballet/txn/fd_txn.h:65
+ACCT_ADDR_MAX = 256       # FD_TXN_ACCT_ADDR_MAX, fd_txn.h:70
+TXN_MAX_SZ = 3570         # FD_TXN_MAX_SZ, fd_txn.h:92
+COUNTERS_RING_SZ = 32
+
+_HDR = struct.Struct("<BBHHBBHHHBBBBH")        # fd_txn_t, 20 bytes
+_INSTR = struct.Struct("<BBHHHH")              # fd_txn_instr_t, 10 bytes
+_LUT = struct.Struct("<HBBHH")                 # fd_txn_acct_addr_lut_t, 8 bytes
+_FIELDS = ("transaction_version", "signature_cnt", "signature_off", "message_off",
+           "readonly_signed_cnt", "readonly_unsigned_cnt", "acct_addr_cnt", "acct_addr_off",
+           "recent_blockhash_off", "addr_table_lookup_cnt", "addr_table_adtl_writable_cnt",
+           "addr_table_adtl_cnt", "_padding_reserved_1", "instr_cnt")
 
 
-def _cu16(b, i):
-    """compact-u16 decode -> (value, next index) or None."""
-    v = 0
-    for k in range(3):
-        if i + k >= len(b):
-            return None
-        c = b[i + k]
-        if k == 2 and c > 3:
-            return None
-        v |= (c & 0x7F) << (7 * k)
-        if not c & 0x80:
-            # reject non-minimal encodings
-            if k > 0 and c == 0:
-                return None
-            return v, i + k + 1
-    return None
+class Counters(ctypes.Structure):
+    """fd_txn_parse_counters_t (src/ballet/txn/fd_txn.h:326-341)."""
+    _fields_ = [("success_cnt", ctypes.c_ulong), ("failure_cnt", ctypes.c_ulong),
+                ("failure_ring", ctypes.c_ulong * COUNTERS_RING_SZ)]
+
+
+def _fn():
+    f = lib().fd_txn_parse
+    f.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+    f.restype = ctypes.c_ulong
+    return f
+
+
+def parse_raw(payload: bytes, counters: Counters | None = None):
+    """-> (footprint, descriptor bytes) with the native parser."""
+    out = ctypes.create_string_buffer(TXN_MAX_SZ)
+    fp = _fn()(bytes(payload), len(payload), out, ctypes.byref(counters) if counters is not None else None)
+    return fp, out.raw[:fp]
+
+
+def decode(raw: bytes) -> dict:
+    t = dict(zip(_FIELDS, _HDR.unpack_from(raw, 0)))
+    t["instr"] = [_INSTR.unpack_from(raw, 20 + 10 * j) for j in range(t["instr_cnt"])]
+    lo = 20 + 10 * t["instr_cnt"]
+    t["luts"] = [_LUT.unpack_from(raw, lo + 8 * j) for j in range(t["addr_table_lookup_cnt"])]
+    t["footprint"] = len(raw)
+    t["raw"] = raw
+    return t
 
 
 def parse(payload: bytes):
-    """-> dict(sig_cnt, sig_off, acct_off, msg_off, version) or None."""
-    b = payload
-    if len(b) > TXN_MTU:
-        return None
-    r = _cu16(b, 0)
-    if r is None:
-        return None
-    sig_cnt, i = r
-    if not 1 <= sig_cnt <= SIG_MAX:
-        return None
-    sig_off = i
-    i += 64 * sig_cnt
-    msg_off = i
-    if i >= len(b):
-        return None
-    version = -1
-    if b[i] & 0x80:
-        version = b[i] & 0x7F
-        if version != 0:
-            return None
-        i += 1
-    if i + 3 > len(b):
-        return None
-    req, ro_signed, ro_unsigned = b[i], b[i + 1], b[i + 2]
-    i += 3
-    if req != sig_cnt or ro_signed >= req:
-        return None
-    r = _cu16(b, i)
-    if r is None:
-        return None
-    acct_cnt, i = r
-    if acct_cnt < req or acct_cnt > ACCT_ADDR_MAX or ro_unsigned > acct_cnt - req:
-        return None
-    acct_off = i
-    i += 32 * acct_cnt + 32  # addresses + recent blockhash
-    if i > len(b):
-        return None
-    r = _cu16(b, i)
-    if r is None:
-        return None
-    instr_cnt, i = r
-    for _ in range(instr_cnt):
-        if i >= len(b):
-            return None
-        i += 1  # program id index
-        for _ in range(2):  # accounts, data
-            r = _cu16(b, i)
-            if r is None:
-                return None
-            n, i = r
-            i += n
-            if i > len(b):
-                return None
-    if version == 0:
-        r = _cu16(b, i)
-        if r is None:
-            return None
-        lut_cnt, i = r
-        for _ in range(lut_cnt):
-            i += 32
-            for _ in range(2):
-                r = _cu16(b, i)
-                if r is None:
-                    return None
-                n, i = r
-                i += n
-                if i > len(b):
-                    return None
-    if i != len(b):
-        return None
-    return {"sig_cnt": sig_cnt, "sig_off": sig_off, "acct_off": acct_off, "msg_off": msg_off, "version": version}
+    fp, raw = parse_raw(payload)
+    return decode(raw) if fp else None
 
 
 def descs_for(payload: bytes, base: int = 0):
@@ -117,8 +77,18 @@ def descs_for(payload: bytes, base: int = 0):
     t = parse(payload)
     if t is None:
         return None
-    d = np.zeros(t["sig_cnt"], DESC_DTYPE)
-    for j in range(t["sig_cnt"]):
-        d[j] = (base + t["sig_off"] + 64 * j, base + t["acct_off"] + 32 * j, base + t["msg_off"],
-                len(payload) - t["msg_off"])
+    k = t["signature_cnt"]
+    d = np.zeros(k, DESC_DTYPE)
+    for j in range(k):
+        d[j] = (base + t["signature_off"] + 64 * j, base + t["acct_addr_off"] + 32 * j,
+                base + t["message_off"], len(payload) - t["message_off"])
     return d
+
+
+def frag(payload: bytes):
+    """QUIC-tile frag for a payload (None if it does not parse)."""
+    fp, raw = parse_raw(payload)
+    if not fp:
+        return None
+    pad = b"\x00" * (len(payload) & 1)
+    return bytes(payload) + pad + raw + struct.pack("<H", len(payload))

@@ -101,8 +101,18 @@ typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
 fd_ed25519_gpu_t *
 fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob );
 
+/* As fd_ed25519_gpu_new with a ring of `depth` (1..8) pinned slots /
+   streams (fd_ed25519_gpu_new uses 3).  More slots keep more batches in
+   flight: a 4096-signature batch occupies 64 of the chip's 1024 SIMDs,
+   so sustained streaming wants several small batches executing at once. */
+fd_ed25519_gpu_t *
+fd_ed25519_gpu_new_ex( int device, unsigned long max_sigs, unsigned long max_blob, int depth );
+
 void
 fd_ed25519_gpu_delete( fd_ed25519_gpu_t * gpu );
+
+unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * gpu );
+unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * gpu );
 
 /* Synchronous: host blob/desc in, host codes out.  Bounds-checks every
    descriptor (FD_ED25519_ERR_ARG in out[i] for a malformed one).
@@ -149,6 +159,20 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
 
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
+
+/* Zero-copy staging: lend the pinned blob (max_blob + 64 bytes) and
+   descriptor (max_sigs) buffers of a free ring slot.  The caller builds
+   the batch in place and passes the same pointers to
+   fd_ed25519_gpu_submit (no host copy), or returns them with
+   fd_ed25519_gpu_unstage.  Returns 0, or FD_ED25519_ERR_ARG if every
+   slot is in flight or lent out (poll first). */
+int
+fd_ed25519_gpu_stage( fd_ed25519_gpu_t *       gpu,
+                      void **                  blob,
+                      fd_ed25519_gpu_desc_t ** desc );
+
+void
+fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * gpu, void const * blob );
 
 /* Diagnostics: fd_ed25519_gpu_verify_dev with HIP events around each of
    the engine's fd_ed25519_gpu_kernel_cnt() kernels on `stream`; blocks

@@ -86,3 +86,35 @@ EXPORT void ref_verify_batch( ulong n, uchar const * sig, uchar const * pub, uch
   }
   if( nthreads > 1 ) for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
 }
+
+/* ---- transaction parser (src/ballet/txn/fd_txn_parse.c) and the HA
+   dedup cache (src/tango/tcache/fd_tcache.h:281-400, header-only
+   macros), for tests/test_txn_parse.py and tests/test_verify_tile.py */
+#include "ballet/txn/fd_txn.h"
+#include "tango/tcache/fd_tcache.h"
+#include <stdlib.h>
+
+EXPORT ulong ref_txn_parse( uchar const * payload, ulong sz, void * out, fd_txn_parse_counters_t * ctr ) {
+  return fd_txn_parse( payload, sz, out, ctr );
+}
+
+typedef struct { ulong depth, map_cnt, oldest; ulong * ring; ulong * map; } ref_tc_t;
+
+EXPORT void * ref_tcache_new( ulong depth, ulong map_cnt ) {
+  ref_tc_t * t = (ref_tc_t *)calloc( 1, sizeof(ref_tc_t) );
+  t->depth = depth; t->map_cnt = map_cnt;
+  t->ring = (ulong *)calloc( depth, sizeof(ulong) );
+  t->map  = (ulong *)calloc( map_cnt, sizeof(ulong) );
+  t->oldest = fd_tcache_reset( t->ring, depth, t->map, map_cnt );
+  return t;
+}
+EXPORT int ref_tcache_insert( void * _t, ulong tag ) {
+  ref_tc_t * t = (ref_tc_t *)_t;
+  int dup;
+  FD_TCACHE_INSERT( dup, t->oldest, t->ring, t->depth, t->map, t->map_cnt, tag );
+  return dup;
+}
+EXPORT void ref_tcache_delete( void * _t ) {
+  ref_tc_t * t = (ref_tc_t *)_t;
+  free( t->ring ); free( t->map ); free( t );
+}

@@ -18,8 +18,10 @@ def declared_functions():
     names = set()
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        inline = set(re.findall(r"static\s+inline[^(]*?\b(fd_[a-z0-9_]+)\s*\(", txt, flags=re.S))
         for m in re.finditer(r"\b(fd_[a-z0-9_]+)\s*\(", txt):
-            names.add(m.group(1))
+            if m.group(1) not in inline:
+                names.add(m.group(1))
     return sorted(names)
 
 
