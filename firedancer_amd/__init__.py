@@ -25,6 +25,9 @@ ERR_MSG = -3
 ERR_ARG = -16
 ERR_GPU = -17
 
+MODE_AVX = 0        # reference AVX2 build semantics (default)
+MODE_PORTABLE = 1   # reference FD_HAS_AVX=0 build semantics
+
 DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"), ("msg_sz", "<u4")])
 
 _lib = None
@@ -129,6 +132,26 @@ def lib() -> ctypes.CDLL:
         L.fd_vt_tcache_insert.restype = ip
         L.fd_vt_tcache_delete.argtypes = [vp]
         L.fd_vt_tcache_delete.restype = None
+        L.fd_ed25519_gpu_sha512_packed.argtypes = [vp, ul, vp, ul, vp, vp, ip]
+        L.fd_ed25519_gpu_sha512_packed.restype = ip
+        L.fd_ed25519_gpu_default.argtypes = []
+        L.fd_ed25519_gpu_default.restype = vp
+        L.fd_ed25519_gpu_set_mode.argtypes = [vp, ip]
+        L.fd_ed25519_gpu_set_mode.restype = ip
+        L.fd_ed25519_gpu_mode.argtypes = [vp]
+        L.fd_ed25519_gpu_mode.restype = ip
+        L.fd_sha512_gpu_batch_new.argtypes = [vp, ip]
+        L.fd_sha512_gpu_batch_new.restype = vp
+        L.fd_sha512_gpu_batch_delete.argtypes = [vp]
+        L.fd_sha512_gpu_batch_delete.restype = None
+        L.fd_sha512_gpu_batch_init.argtypes = [vp]
+        L.fd_sha512_gpu_batch_init.restype = vp
+        L.fd_sha512_gpu_batch_add.argtypes = [vp, vp, ul, vp]
+        L.fd_sha512_gpu_batch_add.restype = vp
+        L.fd_sha512_gpu_batch_fini.argtypes = [vp]
+        L.fd_sha512_gpu_batch_fini.restype = vp
+        L.fd_sha512_gpu_batch_abort.argtypes = [vp]
+        L.fd_sha512_gpu_batch_abort.restype = vp
         _lib = L
     return _lib
 
@@ -206,6 +229,36 @@ class Engine:
         if r < 0:
             raise EngineError(f"poll: {strerror(r)}: {last_error()}")
         return r == 1
+
+    def sha512(self, msgs, is384: bool = False) -> list:
+        """SHA-512 (SHA-384) digests of byte strings on the device."""
+        n = len(msgs)
+        if n == 0:
+            return []
+        offs, parts, o = [], [], 0
+        for m in msgs:
+            offs.append(o)
+            parts.append(bytes(m) + b"\0" * ((-len(m)) % 8))
+            o += len(parts[-1])
+        blob = np.frombuffer(b"".join(parts) + b"\0", np.uint8).copy()
+        desc = np.zeros(n, DESC_DTYPE)
+        desc["msg_off"] = offs
+        desc["msg_sz"] = [len(m) for m in msgs]
+        hsz = 48 if is384 else 64
+        out = np.zeros(n * hsz, np.uint8)
+        err = lib().fd_ed25519_gpu_sha512_packed(self._h, n, _p(blob), o, _p(desc), _p(out), 1 if is384 else 0)
+        if err:
+            raise EngineError(f"sha512_packed: {strerror(err)}: {last_error()}")
+        return [out[i * hsz:(i + 1) * hsz].tobytes() for i in range(n)]
+
+    @property
+    def mode(self) -> int:
+        return lib().fd_ed25519_gpu_mode(self._h)
+
+    @mode.setter
+    def mode(self, m: int) -> None:
+        if lib().fd_ed25519_gpu_set_mode(self._h, m):
+            raise EngineError(f"bad mode {m}")
 
     @property
     def depth(self) -> int:

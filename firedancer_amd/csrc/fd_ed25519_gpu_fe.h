@@ -165,6 +165,49 @@ FD_DEV int fd_fe_isnegative( fd_gpu_fe_t const & f ) {
   return h[0] & 1;
 }
 
+/* z^(p-2) (any exact chain gives the canonical inverse; used only where
+   values, not limbs, are compared: the portable mode's encoding) */
+FD_DEV void fd_fe_invert( fd_gpu_fe_t & out, fd_gpu_fe_t const & z ) {
+  fd_gpu_fe_t t0, t1, t2, t3;
+  fd_fe_sq( t0, z );
+  fd_fe_sq( t1, t0 ); fd_fe_sq( t1, t1 );
+  fd_fe_mul( t1, z, t1 );                                    /* z^9             */
+  fd_fe_mul( t0, t0, t1 );                                   /* z^11            */
+  fd_fe_sq( t2, t0 );
+  fd_fe_mul( t1, t1, t2 );                                   /* 2^5 - 1         */
+  fd_fe_sq( t2, t1 ); for( int i=1; i<5; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t1, t2, t1 );                                   /* 2^10 - 1        */
+  fd_fe_sq( t2, t1 ); for( int i=1; i<10; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t2, t2, t1 );                                   /* 2^20 - 1        */
+  fd_fe_sq( t3, t2 ); for( int i=1; i<20; i++ ) fd_fe_sq( t3, t3 );
+  fd_fe_mul( t2, t3, t2 );                                   /* 2^40 - 1        */
+  for( int i=0; i<10; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t1, t2, t1 );                                   /* 2^50 - 1        */
+  fd_fe_sq( t2, t1 ); for( int i=1; i<50; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t2, t2, t1 );                                   /* 2^100 - 1       */
+  fd_fe_sq( t3, t2 ); for( int i=1; i<100; i++ ) fd_fe_sq( t3, t3 );
+  fd_fe_mul( t2, t3, t2 );                                   /* 2^200 - 1       */
+  for( int i=0; i<50; i++ ) fd_fe_sq( t2, t2 );
+  fd_fe_mul( t1, t2, t1 );                                   /* 2^250 - 1       */
+  for( int i=0; i<5; i++ ) fd_fe_sq( t1, t1 );
+  fd_fe_mul( out, t1, t0 );                                  /* 2^255 - 21      */
+}
+
+/* canonical 32-byte encoding as 8 little-endian words
+   (avx/fd_ed25519_fe.c:48-110 packing) */
+FD_DEV void fd_fe_tobytes32( uint32_t (&w)[8], fd_gpu_fe_t const & f ) {
+  int32_t h[10]; fd_fe_canon( h, f );
+  /* limb i starts at bit ceil(25.5 i) */
+  uint64_t acc = 0; int nb = 0, o = 0;
+#pragma unroll
+  for( int i=0; i<10; i++ ) {
+    acc |= (uint64_t)(uint32_t)h[i] << nb;
+    nb += (i&1) ? 25 : 26;
+    while( nb >= 32 ) { w[o++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+  }
+  w[7] = (uint32_t)acc;   /* 255 bits: the last word holds 31 */
+}
+
 /* fe_frombytes (avx/fd_ed25519_fe.c:4-46): lax, bit 255 ignored,
    non-canonical y >= p accepted.  Input as 8 little-endian
    words. */

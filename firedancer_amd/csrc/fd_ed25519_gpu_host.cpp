@@ -41,6 +41,7 @@ struct fd_ed25519_gpu_slot {
   unsigned long           n;
   unsigned long           ticket;   /* 0 = free */
   int                     staged;   /* pinned buffers lent out by fd_ed25519_gpu_stage */
+  uint8_t *               h_dig;    /* pinned digests (SHA-512 batch), allocated on first use */
 };
 
 struct fd_ed25519_gpu {
@@ -49,6 +50,7 @@ struct fd_ed25519_gpu {
   unsigned long max_blob;
   unsigned long next_ticket;
   int           depth;
+  int           mode;     /* FD_ED25519_GPU_MODE_* */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
@@ -142,6 +144,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     if( sl->h_blob ) hipHostFree( sl->h_blob );
     if( sl->h_desc ) hipHostFree( sl->h_desc );
     if( sl->h_out  ) hipHostFree( sl->h_out );
+    if( sl->h_dig  ) hipHostFree( sl->h_dig );
     if( sl->d_blob ) hipFree( sl->d_blob );
     if( sl->d_desc ) hipFree( sl->d_desc );
     if( sl->d_out  ) hipFree( sl->d_out );
@@ -154,6 +157,14 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
 }
 
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
+
+extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
+  if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE) ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  g->mode = mode;
+  return 0;
+}
+extern "C" int fd_ed25519_gpu_mode( fd_ed25519_gpu_t const * g ) { return g ? g->mode : -1; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
 
@@ -198,7 +209,7 @@ extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n,
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st );
+  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->mode );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   return 0;
 }
@@ -210,7 +221,7 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev );
+  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev, g->mode );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   if( (e = hipEventSynchronize( g->kev[FD_ED25519_GPU_KERNEL_CNT] )) != hipSuccess ) return fd_gpu_fail( "sync", e );
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
@@ -242,7 +253,7 @@ static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsi
     return fd_gpu_fail( "H2D blob", e );
   if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "H2D desc", e );
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream, g->mode )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
@@ -307,6 +318,41 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   return 1;
 }
 
+/* SHA-512 / SHA-384 of n messages blob[msg_off..+msg_sz) (sig_off and
+   pub_off unused) on the device; hash_out receives n digests of 64 (48)
+   bytes back to back.  Synchronous. */
+extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                             fd_ed25519_gpu_desc_t const * desc, void * hash_out, int is384 ) {
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!desc || !hash_out)) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  for( unsigned long i=0; i<n; i++ )
+    if( (unsigned long)desc[i].msg_off + (unsigned long)desc[i].msg_sz > blob_sz ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
+  if( !sl ) return FD_ED25519_ERR_ARG;
+  if( !sl->h_dig && (e = hipHostMalloc( (void **)&sl->h_dig, g->max_sigs * 64UL, hipHostMallocDefault )) != hipSuccess )
+    return fd_gpu_fail( "hipHostMalloc digests", e );
+  if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
+  memset( sl->h_blob + blob_sz, 0, FD_BLOB_PAD );
+  if( sl->h_desc != desc ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  void * d_dig = sl->work.tab;   /* 1280 B per signature of scratch >= 64 B per message */
+  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, blob_sz + FD_BLOB_PAD, hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "H2D blob", e );
+  if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "H2D desc", e );
+  if( (e = fd_ed25519_gpu_launch_sha512( n, sl->d_blob, sl->d_desc, d_dig, is384, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "launch sha512", e );
+  if( (e = hipMemcpyAsync( sl->h_dig, d_dig, n * 64UL, hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "D2H digests", e );
+  if( (e = hipStreamSynchronize( sl->stream )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+  unsigned long hsz = is384 ? 48UL : 64UL;
+  for( unsigned long i=0; i<n; i++ ) memcpy( (uint8_t *)hash_out + i*hsz, sl->h_dig + i*64UL, hsz );
+  sl->staged = 0;
+  return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* Process-default engine and the reference-shaped APIs. */
 
@@ -314,6 +360,9 @@ static std::mutex          fd_default_lock;
 static fd_ed25519_gpu_t *  fd_default_gpu = NULL;
 static unsigned long       fd_default_sigs = 1UL << 16;
 static unsigned long       fd_default_blob = 1UL << 26;
+
+static fd_ed25519_gpu_t * fd_default_engine( void );
+extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_default( void ) { return fd_default_engine(); }
 
 static fd_ed25519_gpu_t * fd_default_engine( void ) {
   std::lock_guard<std::mutex> guard( fd_default_lock );

@@ -320,10 +320,14 @@ FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
 
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-             int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts ) {
+             int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
+             int portable ) {
+  /* portable mode (ref/fd_ed25519_ge.c:242-288 via fd_ed25519_user.c:
+     400-403 with 2POINT 0): only A is decompressed (the grid covers
+     j < n) and there is no small-order test */
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t m = 2*n;
-  if( j >= m ) return;
+  if( j >= (portable ? n : m) ) return;
   uint64_t i = j < n ? j : j - n;
   if( status[i] != FD_ST_PENDING ) { pstat[j] = FD_PT_OK; return; }
   fd_ed25519_gpu_desc_t d = desc[i];
@@ -366,6 +370,8 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
     pts[(uint64_t)(20+k)*m + j] = Z.v[k];
     pts[(uint64_t)(30+k)*m + j] = T.v[k];
   }
+
+  if( portable ) { pstat[j] = FD_PT_OK; return; }
 
   /* small order: [8]P == identity by limb equality */
   fe X2 = x, Y2 = y, Z2 = Z, r[4];
@@ -435,7 +441,8 @@ FD_DEV void fd_conv( fe4 & q, fe4 const & t ) {
 extern "C" __global__ void __launch_bounds__(256, FD_DSM_WAVES)
 fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
           int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-          int32_t * __restrict__ tab, int32_t * __restrict__ out ) {
+          int32_t * __restrict__ tab, int32_t * __restrict__ out,
+          uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   /* lanes past n stay in the wave (the step loop is wave-uniform) but
      read item 0 and store nothing */
@@ -443,7 +450,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   uint64_t ii = live ? i : 0;
   uint64_t m = 2*n;
   int st = status[ii];
-  int pa = pstat[ii], pr = pstat[n+ii];
+  int pa = pstat[ii], pr = portable ? FD_PT_OK : pstat[n+ii];
   int code;
   /* error precedence (fd_ed25519_user.c:372-403) */
   if( st != FD_ST_PENDING )                        code = st;
@@ -556,6 +563,26 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   fd_fe_mul( Y, vt.l[1], vt.l[2] );
   fd_fe_mul( Z, vt.l[2], vt.l[3] );
 
+  if( portable ) {
+    /* canonical encoding of R compared with the signature's r bytes
+       (fd_ed25519_user.c:428-431, ref/fd_ed25519_ge.c:367-375) */
+    fe zi, x, y;
+    fd_fe_invert( zi, Z );
+    fd_fe_mul( x, X, zi );
+    fd_fe_mul( y, Y, zi );
+    uint32_t enc[8];
+    fd_fe_tobytes32( enc, y );
+    enc[7] ^= (uint32_t)fd_fe_isnegative( x ) << 31;
+    uint32_t rw[8];
+    fd_ld32( rw, blob + desc[ii].sig_off );
+    uint32_t diff = 0;
+#pragma unroll
+    for( int k=0; k<8; k++ ) diff |= enc[k] ^ rw[k];
+    if( code == FD_ST_PENDING ) code = diff ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS;
+    if( live ) out[i] = code;
+    return;
+  }
+
   /* compare r.x*R.Z == R.X and r.y*R.Z == R.Y on limbs 0..7 (Q2) */
   fe rx, ry;
 #pragma unroll
@@ -574,6 +601,34 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 }
 
 /* ------------------------------------------------------------------ */
+/* SHA-512 / SHA-384 batch (the ballet batch API's GPU backend,
+   src/ballet/sha512/fd_sha512.h:223-294): one lane per message
+   blob[msg_off..+msg_sz), digest to out[64 i..] (48 bytes for SHA-384). */
+
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_sha512_batch( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+                   uint64_t * __restrict__ out, int is384 ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  fd_ed25519_gpu_desc_t d = desc[i];
+  uint64_t st[8];
+#pragma unroll
+  for( int k=0; k<8; k++ ) st[k] = fd_gpu_sha512_iv[is384 ? 1 : 0][k];
+  fd_sha512_blocks<0>( st, NULL, NULL, blob + d.msg_off, d.msg_sz );
+  int nw = is384 ? 6 : 8;
+#pragma unroll
+  for( int k=0; k<8; k++ ) if( k < nw ) out[8*i + k] = fd_bswap64( st[k] );
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                                    void * out, int is384, hipStream_t stream ) {
+  if( !n ) return hipSuccess;
+  hipLaunchKernelGGL( fd_k_sha512_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                      n, blob, desc, (uint64_t *)out, is384 );
+  return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------ */
 /* Host-side launch (C ABI, used by fd_ed25519_gpu_host.cpp). */
 
 extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
@@ -582,22 +637,24 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
 
 extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                    hipEvent_t const * ev ) {
+                                                    hipEvent_t const * ev, int mode ) {
   if( !n ) return hipSuccess;
+  int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   unsigned nb  = (unsigned)((n + 255) / 256);
-  unsigned nb2 = (unsigned)((2*n + 255) / 256);
+  unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
   hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
   hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start );
   if( ev ) hipEventRecord( ev[1], stream );
-  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts );
+  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable );
   if( ev ) hipEventRecord( ev[2], stream );
-  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out );
+  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
+                      blob, desc, portable );
   if( ev ) hipEventRecord( ev[3], stream );
   return hipGetLastError();
 }
 
 extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
-                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream ) {
-  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL );
+                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode ) {
+  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode );
 }

@@ -91,30 +91,39 @@ FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
   st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
 }
 
-/* SHA-512 of R(32) || A(32) || M(sz), one lane per message.  Each
-   128-byte message block is fetched as 33 aligned dwords and realigned
-   with v_alignbit (words never straddle the R/A/M boundaries: 32 and 64
-   are multiples of 8).  Returns the digest as 8 words where word i holds
-   digest bytes 8i..8i+7 little endian. */
-FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
-  uint64_t st[8] = { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
-                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL };
-  uint64_t L = 64ULL + sz;                           /* bytes hashed */
+/* SHA-512 initial states: SHA-512 and SHA-384 (FIPS 180-4 5.3.5, 5.3.4;
+   src/ballet/sha512/fd_sha512.c:244-263) */
+__constant__ static uint64_t const fd_gpu_sha512_iv[2][8] = {
+  { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+    0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL },
+  { 0xcbbb9d5dc1059ed8ULL, 0x629a292a367cd507ULL, 0x9159015a3070dd17ULL, 0x152fecd8f70e5939ULL,
+    0x67332667ffc00b31ULL, 0x8eb44a8768581511ULL, 0xdb0c2e0d64f98fa7ULL, 0x47b5481dbefa4fa4ULL } };
+
+/* SHA-512 compression over PRE || M(sz), one lane per message, where the
+   PRE-byte prefix (PRE = 64: R || A of an Ed25519 signature; PRE = 0: a
+   plain message) is read from R and A.  Each 128-byte message block is
+   fetched as aligned dwords and realigned with v_alignbit (prefix words
+   never straddle: PRE is a multiple of 8).  st holds the initial state
+   on entry and the final state on return.  Streaming semantics (padding,
+   bit count) of src/ballet/sha512/fd_sha512.c:265-399. */
+template<int PRE>
+FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
+  uint64_t L = (uint64_t)PRE + sz;                   /* bytes hashed */
   uint32_t nblk = (uint32_t)((L + 17ULL + 127ULL) >> 7);
   uint32_t mis = (uint32_t)((uintptr_t)M & 3u);
   uint32_t const * mw = (uint32_t const *)(M - mis);  /* aligned view of M */
   uint32_t sh = mis * 8u;
   for( uint32_t b=0; b<nblk; b++ ) {
     uint64_t w[16];
-    if( b == 0 ) {
+    if( PRE && b == 0 ) {
 #pragma unroll
       for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
 #pragma unroll
       for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
     }
     /* message dwords covering this block's message bytes */
-    int first = b == 0 ? 8 : 0;
-    int64_t mbase = (int64_t)b*128 - 64;             /* message offset of word 0 of this block */
+    int first = b == 0 ? PRE/8 : 0;
+    int64_t mbase = (int64_t)b*128 - PRE;            /* message offset of word 0 of this block */
 #pragma unroll
     for( int i=0; i<16; i++ ) {
       if( i < first ) continue;
@@ -132,7 +141,7 @@ FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const 
           v = ((uint64_t)__builtin_amdgcn_alignbit( q2, q1, sh ) << 32) | __builtin_amdgcn_alignbit( q1, q0, sh );
           v &= (1ULL << (8*keep)) - 1ULL;
         }
-        uint64_t pos = (uint64_t)(mp + 64);
+        uint64_t pos = (uint64_t)(mp + PRE);
         if( pos <= L && L < pos + 8 ) v |= 0x80ULL << (8*(L-pos));
       }
       uint64_t be = fd_bswap64( v );
@@ -141,6 +150,16 @@ FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const 
     }
     fd_sha512_compress( st, w );
   }
+}
+
+/* SHA-512 of R(32) || A(32) || M(sz) (fd_ed25519_user.c:411-414).
+   Returns the digest as 8 words where word i holds digest bytes
+   8i..8i+7 little endian. */
+FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
+  uint64_t st[8];
+#pragma unroll
+  for( int i=0; i<8; i++ ) st[i] = fd_gpu_sha512_iv[0][i];
+  fd_sha512_blocks<64>( st, R, A, M, sz );
 #pragma unroll
   for( int i=0; i<8; i++ ) dig[i] = fd_bswap64( st[i] );
 }

@@ -160,6 +160,20 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 
+/* Reference build whose results the engine reproduces bit for bit:
+     FD_ED25519_GPU_MODE_AVX (default): the AVX2 build the reference's CI
+       uses (FD_HAS_AVX=1): two-point decompression, small-order tests on
+       A and R, non-canonical limb compare;
+     FD_ED25519_GPU_MODE_PORTABLE: the FD_HAS_AVX=0 build: A-only
+       decompression (R off-curve is ERR_MSG, not ERR_PUBKEY), no
+       small-order tests, canonical encoding of R compared with r
+       (fd_ed25519_user.c:400-431 with FD_ED25519_VERIFY_USE_2POINT 0).
+   Applies to batches launched after the call. */
+#define FD_ED25519_GPU_MODE_AVX      (0)
+#define FD_ED25519_GPU_MODE_PORTABLE (1)
+int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * gpu, int mode );
+int fd_ed25519_gpu_mode    ( fd_ed25519_gpu_t const * gpu );
+
 /* Zero-copy staging: lend the pinned blob (max_blob + 64 bytes) and
    descriptor (max_sigs) buffers of a free ring slot.  The caller builds
    the batch in place and passes the same pointers to
@@ -194,6 +208,10 @@ int fd_ed25519_gpu_kernel_cnt( void );
 /* Device the engine runs on; last HIP error string (diagnostics). */
 int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
 char const * fd_ed25519_gpu_last_error( void );
+
+/* The process-default engine behind fd_ed25519_verify (created on first
+   use on $FD_ED25519_GPU_DEVICE, default 0); NULL without a device. */
+fd_ed25519_gpu_t * fd_ed25519_gpu_default( void );
 
 /* Number of usable gfx950 devices visible to this process. */
 int fd_ed25519_gpu_device_cnt( void );

@@ -549,6 +549,16 @@ static void ge_dsm( ge_p2 * out, u8 const * a, ge_p3 const * A, u8 const * b ) {
 }
 
 /* fd_ed25519_verify, AVX2 build (fd_ed25519_user.c:346-433). */
+static void fe_invert( fe * out, fe const * z );
+
+/* PORTABLE_EXACT (the reference's FD_HAS_AVX=0 build,
+   fd_ed25519_user.c:400-431 with FD_ED25519_VERIFY_USE_2POINT 0): S check,
+   single-point decompression of A only (ref/fd_ed25519_ge.c:242-288), no
+   small-order tests, canonical encoding of R compared with r
+   (ref/fd_ed25519_ge.c:367-375).  Group values do not depend on limb
+   trajectories, so the AVX-shaped DSM below yields the same encoding. */
+static int verify_portable( void const * msg, u64 sz, void const * sig, void const * pub );
+
 EXPORT int oracle_verify( void const * msg, u64 sz, void const * sig, void const * pub ) {
   u8 const * r = (u8 const *)sig;
   u8 const * s = r + 32;
@@ -591,6 +601,43 @@ EXPORT int oracle_verify( void const * msg, u64 sz, void const * sig, void const
   return ( memcmp( xz.v, R.X.v, 32 ) | memcmp( yz.v, R.Y.v, 32 ) ) ? -3 : 0;
 }
 
+static int verify_portable( void const * msg, u64 sz, void const * sig, void const * pub ) {
+  u8 const * r = (u8 const *)sig;
+  u8 const * s = r + 32;
+  if( s[31] > 0x10 ) return -1;
+  if( s[31]==0x10 ) {
+    int nz = 0; for( int i=16; i<31; i++ ) nz |= s[i];
+    if( nz ) return 0;
+    static u8 const l_low[16] = { 0xED,0xD3,0xF5,0x5C,0x1A,0x63,0x12,0x58,0xD6,0x9C,0xF7,0xA2,0xDE,0xF9,0xDE,0x14 };
+    int i;
+    for( i=15; i>=0; i-- ) {
+      if( s[i] < l_low[i] ) break;
+      if( s[i] > l_low[i] ) return -1;
+    }
+    if( i<0 ) return -1;
+  }
+  ge_p3 A;
+  if( ge_frombytes_lane( &A, (u8 const *)pub ) ) return -2;
+  fe_neg( &A.X, &A.X );
+  fe_neg( &A.T, &A.T );
+  u8 h[64];
+  sha512_3( h, r, 32, (u8 const *)pub, 32, (u8 const *)msg, sz );
+  oracle_sc_reduce( h, h );
+  ge_p2 R;
+  ge_dsm( &R, h, &A, s );
+  fe zi, x, y;
+  fe_invert( &zi, &R.Z );
+  fe_mul_avx( &x, &R.X, &zi ); fe_mul_avx( &y, &R.Y, &zi );
+  u8 enc[32];
+  fe_tobytes( enc, &y );
+  enc[31] ^= (u8)(fe_isnegative( &x ) << 7);
+  return memcmp( enc, r, 32 ) ? -3 : 0;
+}
+
+EXPORT int oracle_verify_portable( void const * msg, u64 sz, void const * sig, void const * pub ) {
+  return verify_portable( msg, sz, sig, pub );
+}
+
 /* ---------------------------------------------------------------- */
 /* Internals exported for differential tests against the reference. */
 
@@ -610,27 +657,38 @@ EXPORT void oracle_ge_dsm( i32 * out, u8 const * a, i32 const * A, u8 const * b 
    tests: sig[i*64], pub[i*32], msg at data+msg_off[i], msg_sz[i]. */
 typedef struct {
   u64 n; u8 const * sig; u8 const * pub; u8 const * data; u64 const * msg_off; u32 const * msg_sz; i32 * out;
-  u64 lo, hi;
+  u64 lo, hi; int portable;
 } batch_job_t;
 
 static void * batch_worker( void * arg ) {
   batch_job_t * j = (batch_job_t *)arg;
   for( u64 i=j->lo; i<j->hi; i++ )
-    j->out[i] = oracle_verify( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i );
+    j->out[i] = j->portable ? verify_portable( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i )
+                            : oracle_verify  ( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i );
   return NULL;
 }
 
-EXPORT void oracle_verify_batch( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
-                                 u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
+static void verify_batch_mode( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
+                               u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads, int portable ) {
   if( nthreads < 1 ) nthreads = 1;
   if( nthreads > 256 ) nthreads = 256;
   pthread_t th[256]; batch_job_t jobs[256];
   for( int t=0; t<nthreads; t++ ) {
-    jobs[t] = (batch_job_t){ n, sig, pub, data, msg_off, msg_sz, out, n*(u64)t/(u64)nthreads, n*(u64)(t+1)/(u64)nthreads };
+    jobs[t] = (batch_job_t){ n, sig, pub, data, msg_off, msg_sz, out, n*(u64)t/(u64)nthreads, n*(u64)(t+1)/(u64)nthreads, portable };
     if( nthreads==1 ) batch_worker( &jobs[t] );
     else pthread_create( &th[t], NULL, batch_worker, &jobs[t] );
   }
   if( nthreads > 1 ) for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
+}
+
+EXPORT void oracle_verify_batch( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
+                                 u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
+  verify_batch_mode( n, sig, pub, data, msg_off, msg_sz, out, nthreads, 0 );
+}
+
+EXPORT void oracle_verify_batch_portable( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
+                                          u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
+  verify_batch_mode( n, sig, pub, data, msg_off, msg_sz, out, nthreads, 1 );
 }
 
 /* ---------------------------------------------------------------- */

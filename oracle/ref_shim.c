@@ -118,3 +118,5 @@ EXPORT void ref_tcache_delete( void * _t ) {
   ref_tc_t * t = (ref_tc_t *)_t;
   free( t->ring ); free( t->map ); free( t );
 }
+
+EXPORT void ref_sha384( void const * msg, ulong sz, uchar * out ) { fd_sha384_hash( msg, sz, out ); }

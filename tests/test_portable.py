@@ -1,0 +1,77 @@
+"""PORTABLE_EXACT mode: the reference's
+FD_HAS_AVX=0 build -- A-only decompression, no small-order tests,
+canonical encoding of R compared with r (src/ballet/ed25519/
+fd_ed25519_user.c:400-431, ref/fd_ed25519_ge.c:242-288,367-375).
+
+The oracle's restatement (oracle_verify_portable) is pinned here against
+the reference's portable build compiled in place
+(oracle/_ref/libfdref_portable.so); on the GPU the engine in
+MODE_PORTABLE is checked against both."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import firedancer_amd as fa
+from conftest import P, ROOT, ed_vectors, load_corpus, malleability
+from firedancer_amd import corpus
+
+Q2 = ("562c7b301299d47deefe44c5368b77333c214b79b3e7dc03b091f0add168c0910740ac7544423faa742c3ba3d5286c624e1c5174ae4ccad097bea9f3c3cc197f33b0c640b71ae479e30fb2b7159bfb099c9780aa80fff0c1ea9682838b906f8677ea561bef530df8f714bea2b6eeb81b7b468ab64220d9d62a00a557e66bb35d",
+      "a53f00568d07e4944ee86da222b258beae6d8353024faf57de1fa83b05eea496267f66788337eab61e0d36da454c46700ad217fb3cb08d3d016548e4ff5be803",
+      "5bba42a60de96030d8f6a85dc5809e3f39a210671f50ee0ffdab810e18725a49")
+
+
+@pytest.fixture(scope="session")
+def refp():
+    path = os.path.join(ROOT, "oracle", "_ref", "libfdref_portable.so")
+    if not os.path.exists(path):
+        pytest.skip("reference portable build not available")
+    return ctypes.CDLL(path)
+
+
+def codes(L, fn, b):
+    sig, pub, data, off, sz = b.flat()
+    out = np.zeros(len(b), np.int32)
+    getattr(L, fn)(ctypes.c_uint64(len(b)), P(sig), P(pub), P(data), P(off), P(sz), P(out), 8)
+    return out
+
+
+def cases():
+    bs = [load_corpus(n)[0] for n in ("adversarial", "small_order", "msgsizes", "txn1232")]
+    tr = [(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in ed_vectors()]
+    tr += [(b"", s, p) for s, p, _ in malleability()]
+    tr.append((bytes.fromhex(Q2[0]), bytes.fromhex(Q2[1]), bytes.fromhex(Q2[2])))
+    bs.append(corpus.from_triples(tr))
+    bs.append(corpus.adversarial(4000, 200, seed=77, invalid_frac=0.5))
+    return corpus.concat(bs)
+
+
+def test_oracle_portable_vs_reference_portable(oracle, refp):
+    b = cases()
+    a = codes(oracle, "oracle_verify_batch_portable", b)
+    r = codes(refp, "refp_verify_batch", b)
+    assert (a == r).all(), np.nonzero(a != r)[0][:10]
+    # the modes really differ on this corpus (R off-curve, small order, Q2)
+    avx = codes(oracle, "oracle_verify_batch", b)
+    assert (avx != r).sum() > 100
+
+
+@pytest.mark.gpu
+def test_gpu_portable_mode(engine, oracle, refp):
+    b = cases()
+    engine.mode = fa.MODE_PORTABLE
+    try:
+        got = engine.verify_packed(b.blob, b.desc)
+    finally:
+        engine.mode = fa.MODE_AVX
+    r = codes(refp, "refp_verify_batch", b)
+    assert (got == r).all(), np.nonzero(got != r)[0][:10]
+    assert (got == codes(oracle, "oracle_verify_batch_portable", b)).all()
+
+
+@pytest.mark.gpu
+def test_gpu_mode_switch_back(engine, oracle):
+    b = corpus.adversarial(2000, 128, seed=5, invalid_frac=0.5)
+    assert engine.mode == fa.MODE_AVX
+    assert (engine.verify_packed(b.blob, b.desc) == codes(oracle, "oracle_verify_batch", b)).all()
