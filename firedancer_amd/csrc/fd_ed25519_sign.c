@@ -6,8 +6,8 @@
    (src/ballet/ed25519/fd_ed25519.h:40-73).
 
    Field: radix 2^51, 5 x uint64 limbs, unsigned __int128 products.
-   Group: extended twisted Edwards coordinates, fixed-window (4-bit)
-   scalar multiplication of the base point.  Scalars mod L by a 64-bit
+   Group: extended twisted Edwards coordinates, a 64 x 16 fixed-base comb
+   for scalar multiplication of the base point.  Scalars mod L by a 64-bit
    limb Barrett-free schoolbook reduction (bit-serial fold of 2^252). */
 
 #include <stdint.h>
@@ -153,21 +153,25 @@ static void p_add( pt * r, pt const * p, pt const * q ) {
 }
 static void p_zero( pt * r ) { f_set( &r->X, 0 ); f_set( &r->Y, 1 ); f_set( &r->Z, 1 ); f_set( &r->T, 0 ); }
 
-static pt     base_tab[16];
+/* Fixed-base comb: comb[i][j] = j * 16^i * B (i < 64, j < 16), so [a]B
+   is 64 table additions and no doublings. */
+static pt     comb[64][16];
 static pthread_once_t base_once = PTHREAD_ONCE_INIT;
 static void base_init( void ) {
   pt B; B.X = F_BX; B.Y = F_BY; f_set( &B.Z, 1 ); f_mul( &B.T, &F_BX, &F_BY );
-  p_zero( &base_tab[0] );
-  for( int i=1; i<16; i++ ) p_add( &base_tab[i], &base_tab[i-1], &B );
+  for( int i=0; i<64; i++ ) {
+    p_zero( &comb[i][0] );
+    for( int j=1; j<16; j++ ) p_add( &comb[i][j], &comb[i][j-1], &B );
+    for( int k=0; k<4; k++ ) p_add( &B, &B, &B );      /* B <- 16 B */
+  }
 }
 
 static void p_base_mul( pt * r, u8 const * a ) {
   pthread_once( &base_once, base_init );
   pt acc; p_zero( &acc );
-  for( int i=63; i>=0; i-- ) {
-    for( int k=0; k<4; k++ ) p_add( &acc, &acc, &acc );
+  for( int i=0; i<64; i++ ) {
     int nib = (a[i>>1] >> (4*(i&1))) & 15;
-    if( nib ) p_add( &acc, &acc, &base_tab[nib] );
+    if( nib ) p_add( &acc, &acc, &comb[i][nib] );
   }
   *r = acc;
 }
