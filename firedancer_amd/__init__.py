@@ -140,6 +140,18 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_set_mode.restype = ip
         L.fd_ed25519_gpu_mode.argtypes = [vp]
         L.fd_ed25519_gpu_mode.restype = ip
+        L.fd_ed25519_gpu_multi_new.argtypes = [vp, ip, ul, ul]
+        L.fd_ed25519_gpu_multi_new.restype = vp
+        L.fd_ed25519_gpu_multi_delete.argtypes = [vp]
+        L.fd_ed25519_gpu_multi_delete.restype = None
+        L.fd_ed25519_gpu_multi_cnt.argtypes = [vp]
+        L.fd_ed25519_gpu_multi_cnt.restype = ip
+        L.fd_ed25519_gpu_multi_engine.argtypes = [vp, ip]
+        L.fd_ed25519_gpu_multi_engine.restype = vp
+        L.fd_ed25519_gpu_multi_verify_packed.argtypes = [vp, ul, vp, ul, vp, vp]
+        L.fd_ed25519_gpu_multi_verify_packed.restype = ip
+        L.fd_ed25519_codes_to_bitmap.argtypes = [ul, vp, vp]
+        L.fd_ed25519_codes_to_bitmap.restype = None
         L.fd_sha512_gpu_batch_new.argtypes = [vp, ip]
         L.fd_sha512_gpu_batch_new.restype = vp
         L.fd_sha512_gpu_batch_delete.argtypes = [vp]
@@ -263,6 +275,48 @@ class Engine:
     @property
     def depth(self) -> int:
         return lib().fd_ed25519_gpu_depth(self._h)
+
+
+class MultiEngine:
+    """Engines on several devices (repeats allowed) behind one host:
+    fd_ed25519_gpu_multi_t."""
+
+    def __init__(self, devices, max_sigs: int = 1 << 16, max_blob: int = 1 << 26):
+        d = np.ascontiguousarray(devices, np.int32)
+        self._h = lib().fd_ed25519_gpu_multi_new(_p(d), len(d), max_sigs, max_blob)
+        if not self._h:
+            raise EngineError(f"fd_ed25519_gpu_multi_new({list(devices)}) failed: {last_error()}")
+
+    def verify_packed(self, blob: np.ndarray, desc: np.ndarray) -> np.ndarray:
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        out = np.empty(len(desc), dtype=np.int32)
+        err = lib().fd_ed25519_gpu_multi_verify_packed(self._h, len(desc), _p(blob), blob.nbytes, _p(desc), _p(out))
+        if err:
+            raise EngineError(f"multi verify_packed: {strerror(err)}: {last_error()}")
+        return out
+
+    @property
+    def count(self) -> int:
+        return lib().fd_ed25519_gpu_multi_cnt(self._h)
+
+    def close(self):
+        if self._h:
+            lib().fd_ed25519_gpu_multi_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def codes_to_bitmap(codes: np.ndarray) -> np.ndarray:
+    codes = np.ascontiguousarray(codes, np.int32)
+    bm = np.zeros((len(codes) + 7) // 8, np.uint8)
+    lib().fd_ed25519_codes_to_bitmap(len(codes), _p(codes), _p(bm))
+    return bm
 
 
 def verify(msg: bytes, sig: bytes, pub: bytes) -> int:

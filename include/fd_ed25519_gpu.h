@@ -216,6 +216,36 @@ fd_ed25519_gpu_t * fd_ed25519_gpu_default( void );
 /* Number of usable gfx950 devices visible to this process. */
 int fd_ed25519_gpu_device_cnt( void );
 
+/* ---- Multi-device --------------------------------
+
+   Several engines fed by one host: a batch is sharded into contiguous
+   signature ranges, one per engine (ndev entries of devices[], repeats
+   allowed), each engine receives only the blob bytes its shard
+   references, shards run concurrently on per-device host threads, and
+   the codes are gathered into out[] in index order.  No collective: the
+   path has no exchange step.  Same codes and error behaviour as
+   fd_ed25519_gpu_verify_packed. */
+
+typedef struct fd_ed25519_gpu_multi fd_ed25519_gpu_multi_t;
+
+fd_ed25519_gpu_multi_t *
+fd_ed25519_gpu_multi_new( int const * devices, int ndev, unsigned long max_sigs, unsigned long max_blob );
+
+void               fd_ed25519_gpu_multi_delete( fd_ed25519_gpu_multi_t * multi );
+int                fd_ed25519_gpu_multi_cnt   ( fd_ed25519_gpu_multi_t const * multi );
+fd_ed25519_gpu_t * fd_ed25519_gpu_multi_engine( fd_ed25519_gpu_multi_t * multi, int idx );
+
+int
+fd_ed25519_gpu_multi_verify_packed( fd_ed25519_gpu_multi_t *      multi,
+                                    unsigned long                 n,
+                                    void const *                  blob,
+                                    unsigned long                 blob_sz,
+                                    fd_ed25519_gpu_desc_t const * desc,
+                                    int *                         out );
+
+/* Accept bitmap: bit i of bitmap[(n+7)/8] = (codes[i] == FD_ED25519_SUCCESS). */
+void fd_ed25519_codes_to_bitmap( unsigned long n, int const * codes, uint8_t * bitmap );
+
 /* ---- Test-data signer (CPU; not on the verify path) -------------------
    fd_ed25519_public_from_private / fd_ed25519_sign as fd_ed25519.h:40-73:
    RFC 8032 Ed25519.  Provided so benchmarks can build signed synthetic

@@ -76,8 +76,9 @@ def main():
         mism += int((~eq).sum())
         np.add.at(seen, lab, 1)
         np.add.at(agree, lab, eq.astype(np.int64))
-        for c, cnt in zip(*np.unique(np.stack([lab, exp]), axis=1, return_counts=True)):
-            key = f"{corpus.CASES[c[0]]}:{c[1]}"
+        uniq, cnts = np.unique(np.stack([lab, exp]), axis=1, return_counts=True)
+        for c, cnt in zip(uniq.T, cnts):
+            key = f"{corpus.CASES[int(c[0])]}:{int(c[1])}"
             hist[key] = hist.get(key, 0) + int(cnt)
         if k == 0:
             assert list(got[-3:]) == [fa.ERR_MSG] * 3 and list(exp[-3:]) == [fa.ERR_MSG] * 3
