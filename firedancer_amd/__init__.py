@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfd_ed25519_gpu.so")
+LIB_PATH = os.environ.get("FD_ED25519_LIB") or os.path.join(_HERE, "libfd_ed25519_gpu.so")  # override: experiments only
 
 SUCCESS = 0
 ERR_SIG = -1
