@@ -22,7 +22,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define FD_DEV static __device__ __forceinline__
+/* __host__ too: tests/fe_host_harness.cpp runs these exact functions on
+   the CPU against the oracle (tests/test_fe_host.py). */
+#define FD_DEV  static __host__ __device__ __forceinline__
+#define FD_DEVM __host__ __device__ __forceinline__   /* member functions */
 
 typedef struct { int32_t v[10]; } fd_gpu_fe_t;
 typedef struct { fd_gpu_fe_t l[4]; } fd_gpu_fe4_t;
@@ -31,7 +34,22 @@ typedef struct { fd_gpu_fe_t l[4]; } fd_gpu_fe4_t;
    carried limb fits 26 bits).  Without it LLVM rewrites the signed
    products of carried limbs into v_mad_u64_u32 + sign-fix sequences
    (3-4 instructions per product instead of one v_mad_i64_i32). */
-FD_DEV int32_t fd_opaque( int32_t x ) { asm( "" : "+v"(x) ); return x; }
+FD_DEV int32_t fd_opaque( int32_t x ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm( "" : "+v"(x) );
+#endif
+  return x;
+}
+
+/* 64-bit value barrier: pins the bias into the first multiply-accumulate
+   of a column (LLVM otherwise reassociates the constant to the end of the
+   chain and spends a separate 64-bit add on it). */
+FD_DEV int64_t fd_opaque64( int64_t x ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm( "" : "+v"(x) );
+#endif
+  return x;
+}
 
 FD_DEV int32_t fd_sext26( int64_t x ) { return ((int32_t)((uint32_t)x << 6)) >> 6; }
 FD_DEV int32_t fd_sext25( int64_t x ) { return ((int32_t)((uint32_t)x << 7)) >> 7; }
@@ -41,42 +59,151 @@ FD_DEV int32_t fd_sext25( int64_t x ) { return ((int32_t)((uint32_t)x << 7)) >> 
 #define FD_C25(h,n) do { int64_t c_ = ((h) + (1LL<<24)) >> 25; (n) += c_; (h) = (int64_t)fd_sext25( h ); } while(0)
 #define FD_C25X19(h,n) do { int64_t c_ = ((h) + (1LL<<24)) >> 25; (n) += c_*19; (h) = (int64_t)fd_sext25( h ); } while(0)
 
+/* The same 12-step carry chain on BIASED column sums: every column sum
+   arrives with +2^(w-1) already in it (w = 26 for even limbs, 25 for odd;
+   the multiplies start their accumulators at the bias, so it costs
+   nothing).  Then each reference carry c = (h + 2^(w-1)) >> w is a bare
+   shift of the stored value, the residual B - c*2^w is its low w bits,
+   and that residual is again h_new + 2^(w-1) -- so a limb that receives a
+   carry after its own (limbs 4 and 0, round two) is still biased and
+   needs no re-bias.  Limb values are recovered at the end by subtracting
+   the bias (limbs 1 and 5 take their last carry-in after their residual).
+   Exact integer arithmetic throughout, so the limbs are identical to the
+   reference's chain; one 64-bit add per carry fewer. */
+#define FD_B_SHIFT(k) ((k)&1 ? 25 : 26)
+#define FD_BIAS(k)    ((k)&1 ? (1LL<<24) : (1LL<<25))
+#define FD_BC(h,k,n) do { int64_t c_ = (h) >> FD_B_SHIFT(k); (n) += c_; \
+                          (h) = (int64_t)(uint64_t)((uint32_t)(h) & ((1u<<FD_B_SHIFT(k))-1u)); } while(0)
+
 FD_DEV void fd_fe_carry( fd_gpu_fe_t & out, int64_t (&h)[10] ) {
-  FD_C26( h[0], h[1] ); FD_C26( h[4], h[5] );
-  FD_C25( h[1], h[2] ); FD_C25( h[5], h[6] );
-  FD_C26( h[2], h[3] ); FD_C26( h[6], h[7] );
-  FD_C25( h[3], h[4] ); FD_C25( h[7], h[8] );
-  FD_C26( h[4], h[5] ); FD_C26( h[8], h[9] );
-  FD_C25X19( h[9], h[0] );
-  FD_C26( h[0], h[1] );
+  FD_BC( h[0], 0, h[1] ); FD_BC( h[4], 4, h[5] );
+  FD_BC( h[1], 1, h[2] ); FD_BC( h[5], 5, h[6] );
+  FD_BC( h[2], 2, h[3] ); FD_BC( h[6], 6, h[7] );
+  FD_BC( h[3], 3, h[4] ); FD_BC( h[7], 7, h[8] );
+  FD_BC( h[4], 4, h[5] ); FD_BC( h[8], 8, h[9] );
+  { int64_t c_ = h[9] >> 25; h[0] += c_*19; h[9] = (int64_t)(uint64_t)((uint32_t)h[9] & ((1u<<25)-1u)); }
+  FD_BC( h[0], 0, h[1] );
 #pragma unroll
-  for( int i=0; i<10; i++ ) out.v[i] = fd_opaque( (int32_t)h[i] );
+  for( int i=0; i<10; i++ ) out.v[i] = fd_opaque( (int32_t)((uint32_t)h[i] - (uint32_t)FD_BIAS(i)) );
 }
 
-FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return c + (int64_t)a * (int64_t)b; }
+/* One v_mad_i64_i32.  The barrier on the result keeps each column a
+   single serial chain: without it LLVM splits columns into partial chains
+   for ILP and pays a 64-bit add (as costly as a MAC) to merge them; ten
+   independent columns give the scheduler enough parallelism anyway. */
+FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return fd_opaque64( c + (int64_t)a * (int64_t)b ); }
 
-/* h = f*g with the AVX operand convention (fd_ed25519_fe_avx_inl.h:484-590):
-   2*f_odd and 19*g are formed mod 2^32. */
+/* Column sums computed in carry order with the carries ABSORBED into the
+   accumulators (used by fe_mul and fe_sq; limb-identical to
+   fd_fe_carry's chain, tests/test_fe_host.py):
+     - an even column starts at its own bias 2^25 plus 2^50, so its carry
+       (S >> 26) comes out as c + 2^24 = c + (the next odd limb's bias);
+     - the next odd column's multiply chain then STARTS from that value,
+       i.e. "h[k+1] += c" costs nothing;
+     - carries into even columns (c1, c5, c7 -> columns 2, 6, 8) and the
+       round-two carries (c3 -> limb 4, 19 c9 -> limb 0) remain explicit.
+   The per-limb sequence of carry-ins and carry-outs is the reference's
+   (avx/fd_ed25519_fe_avx_inl.h:164-175: 0,4,1,5,2,6,3,7,4,8,9,0): limbs
+   1 and 5 take their last carry-in after their residual, limbs 4 and 0
+   carry twice.  col(k, init) returns init + (column k's products). */
+#define FD_KEVEN ((1LL<<25) + (1LL<<50))
+
+/* COL provides template<int K> int64_t col(int64_t init) const: init +
+   column K's products (a compile-time column index keeps every operand
+   array access static, so nothing is demoted to scratch or LDS). */
+template<typename COL>
+FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
+  /* the even columns wait for no carry: five independent chains first */
+  int64_t S0 = c.template col<0>( FD_KEVEN );
+  int64_t S4 = c.template col<4>( FD_KEVEN );
+  int64_t S2 = c.template col<2>( FD_KEVEN );
+  int64_t S6 = c.template col<6>( FD_KEVEN );
+  int64_t S8 = c.template col<8>( FD_KEVEN );
+  int64_t c0 = S0 >> 26,                  c4 = S4 >> 26;
+  int64_t S1 = c.template col<1>( c0 ),   S5 = c.template col<5>( c4 );
+  int64_t c1 = S1 >> 25,                  c5 = S5 >> 25;
+  S2 += c1;                               S6 += c5;
+  int64_t c2 = S2 >> 26,                  c6 = S6 >> 26;
+  int64_t S3 = c.template col<3>( c2 ),   S7 = c.template col<7>( c6 );
+  int64_t c3 = S3 >> 25,                  c7 = S7 >> 25;
+  S8 += c7;
+  int64_t c8 = S8 >> 26;
+  int64_t S9 = c.template col<9>( c8 );
+  int64_t c9 = S9 >> 25;
+  uint32_t const m26 = (1u<<26)-1u, m25 = (1u<<25)-1u;
+  int64_t  V4  = (int64_t)((uint32_t)S4 & m26) + c3;       /* limb 4: second carry */
+  uint32_t c4b = (uint32_t)(V4 >> 26);
+  int64_t  V0  = (int64_t)((uint32_t)S0 & m26) + c9*19;    /* limb 0: second carry */
+  uint32_t c0b = (uint32_t)(V0 >> 26);
+  out.v[0] = fd_opaque( (int32_t)(((uint32_t)V0 & m26)       - (1u<<25)) );
+  out.v[1] = fd_opaque( (int32_t)(((uint32_t)S1 & m25) + c0b - (1u<<24)) );
+  out.v[2] = fd_opaque( (int32_t)(((uint32_t)S2 & m26)       - (1u<<25)) );
+  out.v[3] = fd_opaque( (int32_t)(((uint32_t)S3 & m25)       - (1u<<24)) );
+  out.v[4] = fd_opaque( (int32_t)(((uint32_t)V4 & m26)       - (1u<<25)) );
+  out.v[5] = fd_opaque( (int32_t)(((uint32_t)S5 & m25) + c4b - (1u<<24)) );
+  out.v[6] = fd_opaque( (int32_t)(((uint32_t)S6 & m26)       - (1u<<25)) );
+  out.v[7] = fd_opaque( (int32_t)(((uint32_t)S7 & m25)       - (1u<<24)) );
+  out.v[8] = fd_opaque( (int32_t)(((uint32_t)S8 & m26)       - (1u<<25)) );
+  out.v[9] = fd_opaque( (int32_t)(((uint32_t)S9 & m25)       - (1u<<24)) );
+}
+
+/* Column functors for fd_fe_chain: fe_mul (AVX MUL convention, 2f_odd and
+   19g pre-scaled) and fe_sq (SQN(1) convention, fd_ed25519_fe_avx_inl.h:
+   592-677: 2f, 19f, 38f). */
+struct fd_mul_cols {
+  int32_t const * f; int32_t const * f2; int32_t const * g; int32_t const * g19;
+  template<int K> FD_DEVM int64_t col( int64_t acc ) const {
+#pragma unroll
+    for( int i=0; i<10; i++ ) {
+      int const j = K - i < 0 ? K - i + 10 : K - i;
+      int32_t a = ((i&1)&(j&1)) ? f2[i] : f[i];
+      acc = fd_mad( a, K - i < 0 ? g19[j] : g[j], acc );
+    }
+    return acc;
+  }
+};
+
+struct fd_sq_cols {
+  int32_t const * F; int32_t const * F2; int32_t const * F19; int32_t const * F38;
+  template<int K> FD_DEVM int64_t col( int64_t a ) const {
+    if( K==0 ) { a=fd_mad(F[0],F[0],a);  a=fd_mad(F2[1],F38[9],a); a=fd_mad(F2[2],F19[8],a); a=fd_mad(F2[3],F38[7],a); a=fd_mad(F2[4],F19[6],a); a=fd_mad(F[5],F38[5],a); }
+    if( K==1 ) { a=fd_mad(F2[0],F[1],a); a=fd_mad(F[2],F38[9],a);  a=fd_mad(F2[3],F19[8],a); a=fd_mad(F[4],F38[7],a);  a=fd_mad(F2[5],F19[6],a); }
+    if( K==2 ) { a=fd_mad(F2[0],F[2],a); a=fd_mad(F2[1],F[1],a);   a=fd_mad(F2[3],F38[9],a); a=fd_mad(F2[4],F19[8],a); a=fd_mad(F2[5],F38[7],a); a=fd_mad(F[6],F19[6],a); }
+    if( K==3 ) { a=fd_mad(F2[0],F[3],a); a=fd_mad(F2[1],F[2],a);   a=fd_mad(F[4],F38[9],a);  a=fd_mad(F2[5],F19[8],a); a=fd_mad(F[6],F38[7],a); }
+    if( K==4 ) { a=fd_mad(F2[0],F[4],a); a=fd_mad(F2[1],F2[3],a);  a=fd_mad(F[2],F[2],a);    a=fd_mad(F2[5],F38[9],a); a=fd_mad(F2[6],F19[8],a); a=fd_mad(F[7],F38[7],a); }
+    if( K==5 ) { a=fd_mad(F2[0],F[5],a); a=fd_mad(F2[1],F[4],a);   a=fd_mad(F2[2],F[3],a);   a=fd_mad(F[6],F38[9],a);  a=fd_mad(F2[7],F19[8],a); }
+    if( K==6 ) { a=fd_mad(F2[0],F[6],a); a=fd_mad(F2[1],F2[5],a);  a=fd_mad(F2[2],F[4],a);   a=fd_mad(F2[3],F[3],a);   a=fd_mad(F2[7],F38[9],a); a=fd_mad(F[8],F19[8],a); }
+    if( K==7 ) { a=fd_mad(F2[0],F[7],a); a=fd_mad(F2[1],F[6],a);   a=fd_mad(F2[2],F[5],a);   a=fd_mad(F2[3],F[4],a);   a=fd_mad(F[8],F38[9],a); }
+    if( K==8 ) { a=fd_mad(F2[0],F[8],a); a=fd_mad(F2[1],F2[7],a);  a=fd_mad(F2[2],F[6],a);   a=fd_mad(F2[3],F2[5],a);  a=fd_mad(F[4],F[4],a);    a=fd_mad(F[9],F38[9],a); }
+    if( K==9 ) { a=fd_mad(F2[0],F[9],a); a=fd_mad(F2[1],F[8],a);   a=fd_mad(F2[2],F[7],a);   a=fd_mad(F2[3],F[6],a);   a=fd_mad(F2[4],F[5],a); }
+    return a;
+  }
+};
+
+/* Operand pre-scales of the AVX MUL convention (fd_ed25519_fe_avx_inl.h:
+   484-590): 2*f for odd limbs and 19*g, formed mod 2^32. */
+FD_DEV void fd_fe_pre_f( int32_t (&f2)[10], fd_gpu_fe_t const & f ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) f2[i] = (i&1) ? fd_opaque( (int32_t)(2u*(uint32_t)f.v[i]) ) : f.v[i];
+}
+FD_DEV void fd_fe_pre_g( int32_t (&g19)[10], fd_gpu_fe_t const & g ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) g19[i] = fd_opaque( (int32_t)(19u*(uint32_t)g.v[i]) );
+}
+
+/* h = f*g from pre-scaled operands (f2 = fd_fe_pre_f(f), g19 = fd_fe_pre_g(g)) */
+FD_DEV void fd_fe_mul_pre( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, int32_t const (&f2)[10],
+                           fd_gpu_fe_t const & g, int32_t const (&g19)[10] ) {
+  fd_mul_cols c = { f.v, f2, g.v, g19 };
+  fd_fe_chain( h, c );
+}
+
+/* h = f*g with the AVX operand convention */
 FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const & g ) {
   int32_t f2[10], g19[10];
-#pragma unroll
-  for( int i=0; i<10; i++ ) {
-    f2[i]  = (i&1) ? fd_opaque( (int32_t)(2u*(uint32_t)f.v[i]) ) : f.v[i];
-    g19[i] = fd_opaque( (int32_t)(19u*(uint32_t)g.v[i]) );
-  }
-  int64_t s[10];
-#pragma unroll
-  for( int k=0; k<10; k++ ) s[k] = 0;
-#pragma unroll
-  for( int i=0; i<10; i++ ) {
-#pragma unroll
-    for( int j=0; j<10; j++ ) {
-      int32_t a = ((i&1)&(j&1)) ? f2[i] : f.v[i];
-      if( i+j<10 ) s[i+j]    = fd_mad( a, g.v[j], s[i+j] );
-      else         s[i+j-10] = fd_mad( a, g19[j], s[i+j-10] );
-    }
-  }
-  fd_fe_carry( h, s );
+  fd_fe_pre_f( f2, f );
+  fd_fe_pre_g( g19, g );
+  fd_fe_mul_pre( h, f, f2, g, g19 );
 }
 
 /* h = n*f^2, n in {1,2}, with the AVX SQN operand convention
@@ -90,17 +217,28 @@ FD_DEV void fd_fe_sqn( fd_gpu_fe_t & h, fd_gpu_fe_t const & fe, int n ) {
     F19[i] = fd_opaque( (int32_t)(19u*(uint32_t)fe.v[i]) );
     F38[i] = fd_opaque( (int32_t)(38u*(uint32_t)fe.v[i]) );
   }
+  if( n==1 ) {
+    /* plain squaring: the SQN(1) column products through the absorbed chain */
+    fd_sq_cols c = { F, F2, F19, F38 };
+    fd_fe_chain( h, c );
+    return;
+  }
+  /* doubled squaring (n == 2): accumulators start at half the carry bias,
+     the sums are doubled, then the plain biased chain */
+  int64_t b[10];
+#pragma unroll
+  for( int k=0; k<10; k++ ) b[k] = n==2 ? FD_BIAS(k)/2 : FD_BIAS(k);
   int64_t s[10];
-  s[0] = fd_mad(F[0],F[0],0);  s[0]=fd_mad(F2[1],F38[9],s[0]); s[0]=fd_mad(F2[2],F19[8],s[0]); s[0]=fd_mad(F2[3],F38[7],s[0]); s[0]=fd_mad(F2[4],F19[6],s[0]); s[0]=fd_mad(F[5],F38[5],s[0]);
-  s[1] = fd_mad(F2[0],F[1],0); s[1]=fd_mad(F[2],F38[9],s[1]);  s[1]=fd_mad(F2[3],F19[8],s[1]); s[1]=fd_mad(F[4],F38[7],s[1]);  s[1]=fd_mad(F2[5],F19[6],s[1]);
-  s[2] = fd_mad(F2[0],F[2],0); s[2]=fd_mad(F2[1],F[1],s[2]);   s[2]=fd_mad(F2[3],F38[9],s[2]); s[2]=fd_mad(F2[4],F19[8],s[2]); s[2]=fd_mad(F2[5],F38[7],s[2]); s[2]=fd_mad(F[6],F19[6],s[2]);
-  s[3] = fd_mad(F2[0],F[3],0); s[3]=fd_mad(F2[1],F[2],s[3]);   s[3]=fd_mad(F[4],F38[9],s[3]);  s[3]=fd_mad(F2[5],F19[8],s[3]); s[3]=fd_mad(F[6],F38[7],s[3]);
-  s[4] = fd_mad(F2[0],F[4],0); s[4]=fd_mad(F2[1],F2[3],s[4]);  s[4]=fd_mad(F[2],F[2],s[4]);    s[4]=fd_mad(F2[5],F38[9],s[4]); s[4]=fd_mad(F2[6],F19[8],s[4]); s[4]=fd_mad(F[7],F38[7],s[4]);
-  s[5] = fd_mad(F2[0],F[5],0); s[5]=fd_mad(F2[1],F[4],s[5]);   s[5]=fd_mad(F2[2],F[3],s[5]);   s[5]=fd_mad(F[6],F38[9],s[5]);  s[5]=fd_mad(F2[7],F19[8],s[5]);
-  s[6] = fd_mad(F2[0],F[6],0); s[6]=fd_mad(F2[1],F2[5],s[6]);  s[6]=fd_mad(F2[2],F[4],s[6]);   s[6]=fd_mad(F2[3],F[3],s[6]);   s[6]=fd_mad(F2[7],F38[9],s[6]); s[6]=fd_mad(F[8],F19[8],s[6]);
-  s[7] = fd_mad(F2[0],F[7],0); s[7]=fd_mad(F2[1],F[6],s[7]);   s[7]=fd_mad(F2[2],F[5],s[7]);   s[7]=fd_mad(F2[3],F[4],s[7]);   s[7]=fd_mad(F[8],F38[9],s[7]);
-  s[8] = fd_mad(F2[0],F[8],0); s[8]=fd_mad(F2[1],F2[7],s[8]);  s[8]=fd_mad(F2[2],F[6],s[8]);   s[8]=fd_mad(F2[3],F2[5],s[8]);  s[8]=fd_mad(F[4],F[4],s[8]);    s[8]=fd_mad(F[9],F38[9],s[8]);
-  s[9] = fd_mad(F2[0],F[9],0); s[9]=fd_mad(F2[1],F[8],s[9]);   s[9]=fd_mad(F2[2],F[7],s[9]);   s[9]=fd_mad(F2[3],F[6],s[9]);   s[9]=fd_mad(F2[4],F[5],s[9]);
+  s[0] = fd_opaque64( fd_mad(F[0],F[0],b[0]) );  s[0]=fd_mad(F2[1],F38[9],s[0]); s[0]=fd_mad(F2[2],F19[8],s[0]); s[0]=fd_mad(F2[3],F38[7],s[0]); s[0]=fd_mad(F2[4],F19[6],s[0]); s[0]=fd_mad(F[5],F38[5],s[0]);
+  s[1] = fd_opaque64( fd_mad(F2[0],F[1],b[1]) ); s[1]=fd_mad(F[2],F38[9],s[1]);  s[1]=fd_mad(F2[3],F19[8],s[1]); s[1]=fd_mad(F[4],F38[7],s[1]);  s[1]=fd_mad(F2[5],F19[6],s[1]);
+  s[2] = fd_opaque64( fd_mad(F2[0],F[2],b[2]) ); s[2]=fd_mad(F2[1],F[1],s[2]);   s[2]=fd_mad(F2[3],F38[9],s[2]); s[2]=fd_mad(F2[4],F19[8],s[2]); s[2]=fd_mad(F2[5],F38[7],s[2]); s[2]=fd_mad(F[6],F19[6],s[2]);
+  s[3] = fd_opaque64( fd_mad(F2[0],F[3],b[3]) ); s[3]=fd_mad(F2[1],F[2],s[3]);   s[3]=fd_mad(F[4],F38[9],s[3]);  s[3]=fd_mad(F2[5],F19[8],s[3]); s[3]=fd_mad(F[6],F38[7],s[3]);
+  s[4] = fd_opaque64( fd_mad(F2[0],F[4],b[4]) ); s[4]=fd_mad(F2[1],F2[3],s[4]);  s[4]=fd_mad(F[2],F[2],s[4]);    s[4]=fd_mad(F2[5],F38[9],s[4]); s[4]=fd_mad(F2[6],F19[8],s[4]); s[4]=fd_mad(F[7],F38[7],s[4]);
+  s[5] = fd_opaque64( fd_mad(F2[0],F[5],b[5]) ); s[5]=fd_mad(F2[1],F[4],s[5]);   s[5]=fd_mad(F2[2],F[3],s[5]);   s[5]=fd_mad(F[6],F38[9],s[5]);  s[5]=fd_mad(F2[7],F19[8],s[5]);
+  s[6] = fd_opaque64( fd_mad(F2[0],F[6],b[6]) ); s[6]=fd_mad(F2[1],F2[5],s[6]);  s[6]=fd_mad(F2[2],F[4],s[6]);   s[6]=fd_mad(F2[3],F[3],s[6]);   s[6]=fd_mad(F2[7],F38[9],s[6]); s[6]=fd_mad(F[8],F19[8],s[6]);
+  s[7] = fd_opaque64( fd_mad(F2[0],F[7],b[7]) ); s[7]=fd_mad(F2[1],F[6],s[7]);   s[7]=fd_mad(F2[2],F[5],s[7]);   s[7]=fd_mad(F2[3],F[4],s[7]);   s[7]=fd_mad(F[8],F38[9],s[7]);
+  s[8] = fd_opaque64( fd_mad(F2[0],F[8],b[8]) ); s[8]=fd_mad(F2[1],F2[7],s[8]);  s[8]=fd_mad(F2[2],F[6],s[8]);   s[8]=fd_mad(F2[3],F2[5],s[8]);  s[8]=fd_mad(F[4],F[4],s[8]);    s[8]=fd_mad(F[9],F38[9],s[8]);
+  s[9] = fd_opaque64( fd_mad(F2[0],F[9],b[9]) ); s[9]=fd_mad(F2[1],F[8],s[9]);   s[9]=fd_mad(F2[2],F[7],s[9]);   s[9]=fd_mad(F2[3],F[6],s[9]);   s[9]=fd_mad(F2[4],F[5],s[9]);
   if( n==2 ) {
 #pragma unroll
     for( int k=0; k<10; k++ ) s[k] += s[k];

@@ -81,7 +81,7 @@ extern "C" int fd_ed25519_gpu_device_cnt( void ) {
 
 static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long N ) {
   uint8_t * p = (uint8_t *)base;
-  w->tab      = (int32_t *)p; p += 1280UL * N;
+  w->tab      = (int32_t *)p; p += 4UL * FD_TAB_SIG * N;
   w->pts      = (int32_t *)p; p +=  320UL * N;
   w->status   = (int32_t *)p; p +=    4UL * N;
   w->pstat    = (int32_t *)p; p +=    8UL * N;
@@ -337,7 +337,7 @@ extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long
   if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
   memset( sl->h_blob + blob_sz, 0, FD_BLOB_PAD );
   if( sl->h_desc != desc ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
-  void * d_dig = sl->work.tab;   /* 1280 B per signature of scratch >= 64 B per message */
+  void * d_dig = sl->work.tab;   /* 1536 B per signature of scratch >= 64 B per message */
   if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, blob_sz + FD_BLOB_PAD, hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "H2D blob", e );
   if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )

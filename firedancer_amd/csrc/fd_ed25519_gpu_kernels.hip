@@ -35,7 +35,10 @@ typedef fd_gpu_fe4_t fe4;
 #define FD_PT_BAD      1   /* not on curve           -> ERR_PUBKEY */
 #define FD_PT_SMALL    2   /* small order            -> A: ERR_PUBKEY, R: ERR_SIG */
 
-__constant__ static fe4 fd_gpu_bi_precomp[8];
+/* Bi = (2i+1)B in cached form, padded to the Ai table's entry layout
+   [lane 4][FD_TAB_LANE], so an add step loads its entry the same way
+   whichever table it comes from */
+__device__ static int32_t fd_gpu_bi_tab[8*FD_TAB_ENTRY];
 
 /* minimum waves per SIMD requested for fd_k_dsm (caps its VGPRs) */
 #ifndef FD_DSM_WAVES
@@ -396,29 +399,27 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
    multiples of -A in cached form) is kept in a per-signature SoA scratch
    table [8][4][10][n] in HBM (L2-resident while the launch runs). */
 
-/* Per-signature Ai table, AoS: tab[sig][entry][lane][limb] int32, one
-   160-byte entry per (sig, e).  An add step reads one whole entry of its
-   own signature as 10 x 16-byte loads; with the SoA layout each active
-   lane would touch 40 separate cache lines (measured 21 GB fetched per
-   262K-signature launch). */
+/* Per-signature Ai table, AoS: tab[sig][entry][lane][12] int32 (10 limbs,
+   2 pad), one 192-byte entry per (sig, e).  An add step reads the four
+   lanes of one entry of its own signature as 3 x 16-byte loads each; with
+   a SoA layout each active lane would touch 40 separate cache lines
+   (measured 21 GB fetched per 262K-signature launch). */
 FD_DEV void fd_tab_store( int32_t * tab, uint64_t i, int e, fe4 const & v ) {
-  int4 * p = (int4 *)(tab + i*320 + (uint64_t)e*40);
+  int32_t * p = tab + i*FD_TAB_SIG + (uint64_t)e*FD_TAB_ENTRY;
 #pragma unroll
-  for( int c=0; c<10; c++ ) {
-    int q = 4*c;
-    p[c] = make_int4( v.l[(q+0)/10].v[(q+0)%10], v.l[(q+1)/10].v[(q+1)%10],
-                      v.l[(q+2)/10].v[(q+2)%10], v.l[(q+3)/10].v[(q+3)%10] );
+  for( int l=0; l<4; l++ ) {
+    int4 * q = (int4 *)(p + l*FD_TAB_LANE);
+    q[0] = make_int4( v.l[l].v[0], v.l[l].v[1], v.l[l].v[2], v.l[l].v[3] );
+    q[1] = make_int4( v.l[l].v[4], v.l[l].v[5], v.l[l].v[6], v.l[l].v[7] );
+    q[2] = make_int4( v.l[l].v[8], v.l[l].v[9], 0, 0 );
   }
 }
-FD_DEV void fd_tab_load( fe4 & v, int32_t const * tab, uint64_t i, int e ) {
-  int4 const * p = (int4 const *)(tab + i*320 + (uint64_t)e*40);
-#pragma unroll
-  for( int c=0; c<10; c++ ) {
-    int4 x = p[c];
-    int q = 4*c;
-    v.l[(q+0)/10].v[(q+0)%10] = x.x; v.l[(q+1)/10].v[(q+1)%10] = x.y;
-    v.l[(q+2)/10].v[(q+2)%10] = x.z; v.l[(q+3)/10].v[(q+3)%10] = x.w;
-  }
+FD_DEV void fd_tab_lane( fe & v, int32_t const * p ) {
+  int4 const * q = (int4 const *)p;
+  int4 a = q[0], b = q[1], c = q[2];
+  v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
+  v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
+  v.v[8] = c.x; v.v[9] = c.y;
 }
 
 FD_DEV int fd_wave_min( int x ) {
@@ -430,12 +431,17 @@ FD_DEV int fd_wave_min( int x ) {
 /* p1p1 -> p3 conversion, lanes [Z, Y, X, T] = [t2*t3, t1*t2, t0*t3, t0*t1]:
    operand for operand the reference's MUL(perm(vt,2,1,0,0),
    perm(vt,3,2,3,1)) (avx/fd_ed25519_ge.c:506-508); its lanes Z, Y, X are
-   also the p1p1 -> p2 conversion MUL(vt, perm(vt,3,2,3,3)) (:521-522). */
-FD_DEV void fd_conv( fe4 & q, fe4 const & t ) {
-  fd_fe_mul( q.l[0], t.l[2], t.l[3] );
-  fd_fe_mul( q.l[1], t.l[1], t.l[2] );
-  fd_fe_mul( q.l[2], t.l[0], t.l[3] );
-  fd_fe_mul( q.l[3], t.l[0], t.l[1] );
+   also the p1p1 -> p2 conversion MUL(vt, perm(vt,3,2,3,3)) (:521-522).
+   The operand pre-scales shared between the four products (19 t3, 2 t0)
+   are formed once. */
+FD_DEV void fd_conv( fe & Z, fe & Y, fe & X, fe & T, fe4 const & t ) {
+  int32_t g3[10], f0[10];
+  fd_fe_pre_g( g3, t.l[3] );
+  fd_fe_pre_f( f0, t.l[0] );
+  { int32_t f2[10]; fd_fe_pre_f( f2, t.l[2] ); fd_fe_mul_pre( Z, t.l[2], f2, t.l[3], g3 ); }
+  fd_fe_mul_pre( X, t.l[0], f0, t.l[3], g3 );
+  { int32_t f1[10], g2[10]; fd_fe_pre_f( f1, t.l[1] ); fd_fe_pre_g( g2, t.l[2] ); fd_fe_mul_pre( Y, t.l[1], f1, t.l[2], g2 ); }
+  { int32_t g1[10]; fd_fe_pre_g( g1, t.l[1] ); fd_fe_mul_pre( T, t.l[0], f0, t.l[1], g1 ); }
 }
 
 extern "C" __global__ void __launch_bounds__(256, FD_DSM_WAVES)
@@ -497,64 +503,92 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   }
 
   /* Main loop as a per-lane op stream (avx/fd_ed25519_ge.c:488-523
-     restated).  Every step converts the p1p1 state to p3 (4 multiplies)
-     and applies its op -- D: DBL_MIX(SQN([X+Y,Y,X,Z]; 1,1,1,2)), the
-     squarings issued as multiplies f*f and Z*(2Z) (identical column sums
-     for these operand ranges); A:
-     SUB_MIX(MUL(SUBADD_12(p3), entry)) with the entry's lanes 1,2
-     swapped for a negative digit and the result's lanes 2,3 swapped for
-     a positive one.  All lanes run the same instructions on different
-     operands.  The initial p1p1 [0,1,1,1] converts to the identity. */
+     restated).  Every step converts the p1p1 state to p3 (4 multiplies,
+     [Z,Y,X,T]) and applies its op with four more multiplies whose
+     operands are selected per lane (same operand roles as the reference):
+
+                 D: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2))   A: SUB_MIX(MUL(SUBADD_12(p3), E))
+       P = f*g   (X+Y)*(X+Y)                            (Y+X)*E2
+       Q         Z*(2Z)                                 Z*E0
+       R         Y*Y                                    (Y-X)*E1
+       S         X*X                                    T*E3
+       out       [P-R-S, R+S, R-S, Q-R+S]               [P-R, P+R, 2Q-S, 2Q+S]
+
+     E is the signed digit's table entry; a negative digit swaps its lanes
+     1,2 (here: by swapping the two load addresses) and a positive one swaps
+     out lanes 2,3.  The squarings are issued as multiplies f*f and Z*(2Z)
+     (identical column sums).  All lanes run the same
+     instructions on different operands.  The initial p1p1 [0,1,1,1]
+     converts to the identity. */
 #pragma unroll
   for( int l=0; l<4; l++ ) fd_fe_set( vt.l[l], l ? 1 : 0 );
+  int32_t const * tab_i = tab + ii*FD_TAB_SIG;
   int t0 = fd_wave_min( start );
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
     int op = (t >= start) ? (int)ops[(uint64_t)t*n + ii] : 0;
     int is_add = op & FD_OP_ADD;
     int e   = op & 7;
     int neg = (op >> 5) & 1;
-    fe4 q; fd_conv( q, vt );   /* q = [Z, Y, X, T] */
-    /* operands of the op's four multiplies, built lane by lane; the table
-       entry is read lane by lane by add steps only (the Ai table does not
-       fit the caches at full batch size, so D steps must not touch it) */
-    fe4 ent;
-    if( op & 0x40 )  ent = fd_gpu_bi_precomp[e];
-    else if( is_add ) fd_tab_load( ent, tab, ii, e );
-    else {
-#pragma unroll
-      for( int l=0; l<4; l++ ) fd_fe_set( ent.l[l], 0 );
+    fe Z, Y, X, T; fd_conv( Z, Y, X, T, vt );
+
+    /* the table entry is read by add steps only (the Ai table does not fit
+       the caches at full batch size, so D steps must not touch it) */
+    fe E0, E1, E2, E3;
+    if( is_add ) {
+      int32_t const * ent = ((op & 0x40) ? fd_gpu_bi_tab : tab_i) + e*FD_TAB_ENTRY;
+      fd_tab_lane( E0, ent );
+      fd_tab_lane( E1, ent + (neg ? 2 : 1)*FD_TAB_LANE );
+      fd_tab_lane( E2, ent + (neg ? 1 : 2)*FD_TAB_LANE );
+      fd_tab_lane( E3, ent + 3*FD_TAB_LANE );
     }
-    fe4 h;
+    fe h0, h1, h2, h3;   /* P, Q, R, S */
+    {
+      fe xy, g;
 #pragma unroll
-    for( int l=0; l<4; l++ ) {
-      /* entry lane: lanes 1,2 swapped for a negative digit */
+      for( int k=0; k<10; k++ ) {
+        xy.v[k] = (int32_t)((uint32_t)X.v[k] + (uint32_t)Y.v[k]);
+        g.v[k]  = is_add ? E2.v[k] : xy.v[k];
+      }
+      fd_fe_mul( h0, xy, g );
+    }
+    {
+      fe g;
+#pragma unroll
+      for( int k=0; k<10; k++ ) g.v[k] = is_add ? E0.v[k] : (int32_t)(2u*(uint32_t)Z.v[k]);
+      fd_fe_mul( h1, Z, g );
+    }
+    {
       fe f, g;
 #pragma unroll
       for( int k=0; k<10; k++ ) {
-        uint32_t z = q.l[0].v[k], y = q.l[1].v[k], x = q.l[2].v[k], t = q.l[3].v[k];
-        uint32_t fa, fd, gd;
-        int32_t  ga;
-        if( l==0 ) { fa = z;   fd = x+y; gd = x+y;  ga = ent.l[0].v[k]; }
-        if( l==1 ) { fa = y-x; fd = y;   gd = y;    ga = neg ? ent.l[2].v[k] : ent.l[1].v[k]; }
-        if( l==2 ) { fa = y+x; fd = x;   gd = x;    ga = neg ? ent.l[1].v[k] : ent.l[2].v[k]; }
-        if( l==3 ) { fa = t;   fd = z;   gd = 2u*z; ga = ent.l[3].v[k]; }
-        f.v[k] = (int32_t)(is_add ? fa : fd);
-        g.v[k] = is_add ? ga : (int32_t)gd;
+        f.v[k] = is_add ? (int32_t)((uint32_t)Y.v[k] - (uint32_t)X.v[k]) : Y.v[k];
+        g.v[k] = is_add ? E1.v[k] : Y.v[k];
       }
-      fd_fe_mul( h.l[l], f, g );
+      fd_fe_mul( h2, f, g );
     }
-    /* D: [a-b-c, b+c, b-c, d-b+c]; A: [c-b, c+b, 2a-d, 2a+d] with lanes
-       2,3 swapped for a positive digit */
+    {
+      fe f, g;
+#pragma unroll
+      for( int k=0; k<10; k++ ) {
+        f.v[k] = is_add ? T.v[k]  : X.v[k];
+        g.v[k] = is_add ? E3.v[k] : X.v[k];
+      }
+      fd_fe_mul( h3, f, g );
+    }
     int pos = is_add && !neg;
 #pragma unroll
     for( int k=0; k<10; k++ ) {
-      uint32_t a=h.l[0].v[k], b=h.l[1].v[k], c=h.l[2].v[k], d=h.l[3].v[k];
-      uint32_t d0 = a-b-c, d1 = b+c, d2 = b-c, d3 = d-b+c;
-      uint32_t a0 = c-b,   a1 = c+b, a2 = 2u*a-d, a3 = 2u*a+d;
-      vt.l[0].v[k] = (int32_t)(is_add ? a0 : d0);
-      vt.l[1].v[k] = (int32_t)(is_add ? a1 : d1);
-      vt.l[2].v[k] = (int32_t)(is_add ? (pos ? a3 : a2) : d2);
-      vt.l[3].v[k] = (int32_t)(is_add ? (pos ? a2 : a3) : d3);
+      uint32_t P = h0.v[k], Q = h1.v[k], R = h2.v[k], S = h3.v[k];
+      uint32_t PR = P - R, Q2 = 2u*Q;
+      uint32_t o0 = PR - (is_add ? 0u : S);
+      uint32_t o1 = R + (is_add ? P : S);
+      uint32_t u  = is_add ? Q2 : R;            /* o2 = u - S */
+      uint32_t w  = is_add ? Q2 : Q - R;        /* o3 = w + S */
+      uint32_t o2 = u - S, o3 = w + S;
+      vt.l[0].v[k] = (int32_t)o0;
+      vt.l[1].v[k] = (int32_t)o1;
+      vt.l[2].v[k] = (int32_t)(pos ? o3 : o2);
+      vt.l[3].v[k] = (int32_t)(pos ? o2 : o3);
     }
   }
   /* final p1p1 -> p2 */
@@ -632,7 +666,12 @@ extern "C" hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * 
 /* Host-side launch (C ABI, used by fd_ed25519_gpu_host.cpp). */
 
 extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
-  return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_precomp), FD_GPU_BI_PRECOMP, sizeof(FD_GPU_BI_PRECOMP) );
+  static int32_t bi[8*FD_TAB_ENTRY];
+  for( int e=0; e<8; e++ )
+    for( int l=0; l<4; l++ )
+      for( int k=0; k<FD_TAB_LANE; k++ )
+        bi[e*FD_TAB_ENTRY + l*FD_TAB_LANE + k] = k < 10 ? FD_GPU_BI_PRECOMP[e].l[l].v[k] : 0;
+  return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_tab), bi, sizeof(bi) );
 }
 
 extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,

@@ -11,7 +11,8 @@
      op_start int32 [N]          first op index (FD_OPS_MAX if none)
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
-     tab      int32 [N][320]     per-signature Ai table (8 x 4 lanes x 10), AoS */
+     tab      int32 [N][384]     per-signature Ai table, AoS [entry 8][lane 4][12]
+                                 (10 limbs + 2 pad: 48-byte lanes, 16-byte aligned) */
 typedef struct fd_ed25519_gpu_work {
   int32_t * status;
   uint8_t * ops;
@@ -28,7 +29,12 @@ typedef struct fd_ed25519_gpu_work {
 /* op stream capacity: 256 doublings + at most 256 adds per scalar */
 #define FD_OPS_MAX 768
 
-#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 4UL + (unsigned long)FD_OPS_MAX + 8UL + 320UL + 1280UL)
+/* Ai / Bi table entry geometry (dwords) */
+#define FD_TAB_LANE  12
+#define FD_TAB_ENTRY (4*FD_TAB_LANE)
+#define FD_TAB_SIG   (8*FD_TAB_ENTRY)
+
+#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 4UL + (unsigned long)FD_OPS_MAX + 8UL + 320UL + 4UL*(unsigned long)FD_TAB_SIG)
 
 #ifdef __cplusplus
 extern "C" {

@@ -1,0 +1,41 @@
+// fe_host_harness.cpp -- runs the device field arithmetic of
+// firedancer_amd/csrc/fd_ed25519_gpu_fe.h on the host CPU (its functions are
+// __host__ __device__) so tests/test_fe_host.py can compare them limb for
+// limb with the oracle's restatement of the reference's AVX field path.
+// Test infrastructure only.
+#include "fd_ed25519_gpu_fe.h"
+
+extern "C" {
+void h_fe_mul( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, b, c;
+    for( int k=0; k<10; k++ ) { a.v[k] = f[10*i+k]; b.v[k] = g[10*i+k]; }
+    fd_fe_mul( c, a, b );
+    for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
+void h_fe_sqn( int32_t * h, int32_t const * f, int nsq, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, c;
+    for( int k=0; k<10; k++ ) a.v[k] = f[10*i+k];
+    fd_fe_sqn( c, a, nsq );
+    for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
+void h_fe_tobytes32( uint32_t * w, int32_t const * f, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a; uint32_t o[8];
+    for( int k=0; k<10; k++ ) a.v[k] = f[10*i+k];
+    fd_fe_tobytes32( o, a );
+    for( int k=0; k<8; k++ ) w[8*i+k] = o[k];
+  }
+}
+void h_fe_invert( int32_t * h, int32_t const * f, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, c;
+    for( int k=0; k<10; k++ ) a.v[k] = f[10*i+k];
+    fd_fe_invert( c, a );
+    for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
+}
