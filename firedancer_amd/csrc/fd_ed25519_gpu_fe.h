@@ -51,6 +51,9 @@ FD_DEV int64_t fd_opaque64( int64_t x ) {
   return x;
 }
 
+/* m ? a : b bitwise for a lane mask m in {0, ~0} (v_bfi_b32) */
+FD_DEV uint32_t fd_sel( uint32_t m, uint32_t a, uint32_t b ) { return (a & m) | (b & ~m); }
+
 FD_DEV int32_t fd_sext26( int64_t x ) { return ((int32_t)((uint32_t)x << 6)) >> 6; }
 FD_DEV int32_t fd_sext25( int64_t x ) { return ((int32_t)((uint32_t)x << 7)) >> 7; }
 
@@ -108,28 +111,12 @@ FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return fd_opaque64( c
    carry twice.  col(k, init) returns init + (column k's products). */
 #define FD_KEVEN ((1LL<<25) + (1LL<<50))
 
-/* COL provides template<int K> int64_t col(int64_t init) const: init +
-   column K's products (a compile-time column index keeps every operand
-   array access static, so nothing is demoted to scratch or LDS). */
-template<typename COL>
-FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
-  /* the even columns wait for no carry: five independent chains first */
-  int64_t S0 = c.template col<0>( FD_KEVEN );
-  int64_t S4 = c.template col<4>( FD_KEVEN );
-  int64_t S2 = c.template col<2>( FD_KEVEN );
-  int64_t S6 = c.template col<6>( FD_KEVEN );
-  int64_t S8 = c.template col<8>( FD_KEVEN );
-  int64_t c0 = S0 >> 26,                  c4 = S4 >> 26;
-  int64_t S1 = c.template col<1>( c0 ),   S5 = c.template col<5>( c4 );
-  int64_t c1 = S1 >> 25,                  c5 = S5 >> 25;
-  S2 += c1;                               S6 += c5;
-  int64_t c2 = S2 >> 26,                  c6 = S6 >> 26;
-  int64_t S3 = c.template col<3>( c2 ),   S7 = c.template col<7>( c6 );
-  int64_t c3 = S3 >> 25,                  c7 = S7 >> 25;
-  S8 += c7;
-  int64_t c8 = S8 >> 26;
-  int64_t S9 = c.template col<9>( c8 );
-  int64_t c9 = S9 >> 25;
+/* limbs from the absorbed-chain column sums (S2, S6, S8 with their
+   carry-ins added): round-two carries c3 -> limb 4, 19 c9 -> limb 0, the
+   residuals, the biases removed */
+FD_DEV void fd_fe_limbs( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, int64_t S3, int64_t S4,
+                         int64_t S5, int64_t S6, int64_t S7, int64_t S8, int64_t S9 ) {
+  int64_t c3 = S3 >> 25, c9 = S9 >> 25;
   uint32_t const m26 = (1u<<26)-1u, m25 = (1u<<25)-1u;
   int64_t  V4  = (int64_t)((uint32_t)S4 & m26) + c3;       /* limb 4: second carry */
   uint32_t c4b = (uint32_t)(V4 >> 26);
@@ -147,19 +134,90 @@ FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
   out.v[9] = fd_opaque( (int32_t)(((uint32_t)S9 & m25)       - (1u<<24)) );
 }
 
+/* COL provides template<int K> int64_t col(int64_t init) const: init +
+   column K's products (a compile-time column index keeps every operand
+   array access static, so nothing is demoted to scratch or LDS). */
+template<typename COL>
+FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
+  /* the even columns wait for no carry: five independent chains first */
+  int64_t S0 = c.template col<0>( FD_KEVEN );
+  int64_t S4 = c.template col<4>( FD_KEVEN );
+  int64_t S2 = c.template col<2>( FD_KEVEN );
+  int64_t S6 = c.template col<6>( FD_KEVEN );
+  int64_t S8 = c.template col<8>( FD_KEVEN );
+  int64_t c0 = S0 >> 26,                  c4 = S4 >> 26;
+  int64_t S1 = c.template col<1>( c0 ),   S5 = c.template col<5>( c4 );
+  int64_t c1 = S1 >> 25,                  c5 = S5 >> 25;
+  S2 += c1;                               S6 += c5;
+  int64_t c2 = S2 >> 26,                  c6 = S6 >> 26;
+  int64_t S3 = c.template col<3>( c2 ),   S7 = c.template col<7>( c6 );
+  S8 += S7 >> 25;
+  int64_t c8 = S8 >> 26;
+  int64_t S9 = c.template col<9>( c8 );
+  fd_fe_limbs( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
+}
+
+/* fd_fe_chain for two independent products (fd_mul_cols2), carries and
+   limb recovery as above, the column chains of the two interleaved. */
+template<typename COL2>
+FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, COL2 const & c ) {
+  int64_t a0 = FD_KEVEN, b0 = FD_KEVEN, a4 = FD_KEVEN, b4 = FD_KEVEN;
+  c.template col2<0,4>( a0, b0, a4, b4 );
+  int64_t a2 = FD_KEVEN, b2 = FD_KEVEN, a6 = FD_KEVEN, b6 = FD_KEVEN;
+  c.template col2<2,6>( a2, b2, a6, b6 );
+  int64_t a8 = FD_KEVEN, b8 = FD_KEVEN, a1 = a0 >> 26, b1 = b0 >> 26;
+  c.template col2<8,1>( a8, b8, a1, b1 );
+  a2 += a1 >> 25; b2 += b1 >> 25;
+  int64_t a5 = a4 >> 26, b5 = b4 >> 26, a3 = a2 >> 26, b3 = b2 >> 26;
+  c.template col2<5,3>( a5, b5, a3, b3 );
+  a6 += a5 >> 25; b6 += b5 >> 25;
+  int64_t a7 = a6 >> 26, b7 = b6 >> 26;
+  c.template col<7>( a7, b7 );
+  a8 += a7 >> 25; b8 += b7 >> 25;
+  int64_t a9 = a8 >> 26, b9 = b8 >> 26;
+  c.template col<9>( a9, b9 );
+  fd_fe_limbs( oa, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
+  fd_fe_limbs( ob, b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+}
+
 /* Column functors for fd_fe_chain: fe_mul (AVX MUL convention, 2f_odd and
    19g pre-scaled) and fe_sq (SQN(1) convention, fd_ed25519_fe_avx_inl.h:
    592-677: 2f, 19f, 38f). */
 struct fd_mul_cols {
   int32_t const * f; int32_t const * f2; int32_t const * g; int32_t const * g19;
+  template<int K, int I> FD_DEVM int64_t term( int64_t acc ) const {
+    int const j = K - I < 0 ? K - I + 10 : K - I;
+    return fd_mad( ((I&1)&(j&1)) ? f2[I] : f[I], K - I < 0 ? g19[j] : g[j], acc );
+  }
   template<int K> FD_DEVM int64_t col( int64_t acc ) const {
-#pragma unroll
-    for( int i=0; i<10; i++ ) {
-      int const j = K - i < 0 ? K - i + 10 : K - i;
-      int32_t a = ((i&1)&(j&1)) ? f2[i] : f[i];
-      acc = fd_mad( a, K - i < 0 ? g19[j] : g[j], acc );
-    }
+    acc = term<K,0>( acc ); acc = term<K,1>( acc ); acc = term<K,2>( acc ); acc = term<K,3>( acc ); acc = term<K,4>( acc );
+    acc = term<K,5>( acc ); acc = term<K,6>( acc ); acc = term<K,7>( acc ); acc = term<K,8>( acc ); acc = term<K,9>( acc );
     return acc;
+  }
+};
+
+/* Two independent products through the same chain with their column
+   multiply chains interleaved term by term.  A v_mad_i64_i32 whose 64-bit
+   accumulator was written by one of the previous two VALU instructions
+   costs hazard wait states (s_nop), so two columns of each product run
+   together where the carry order allows (col2: four chains, every MAC
+   three instructions after the one it depends on). */
+struct fd_mul_cols2 {
+  fd_mul_cols a, b;
+  template<int K, int I> FD_DEVM void t1( int64_t & sa, int64_t & sb ) const {
+    sa = a.term<K,I>( sa ); sb = b.term<K,I>( sb );
+  }
+  template<int K> FD_DEVM void col( int64_t & sa, int64_t & sb ) const {
+    t1<K,0>( sa, sb ); t1<K,1>( sa, sb ); t1<K,2>( sa, sb ); t1<K,3>( sa, sb ); t1<K,4>( sa, sb );
+    t1<K,5>( sa, sb ); t1<K,6>( sa, sb ); t1<K,7>( sa, sb ); t1<K,8>( sa, sb ); t1<K,9>( sa, sb );
+  }
+  template<int K, int L, int I> FD_DEVM void t2( int64_t & sa, int64_t & sb, int64_t & ua, int64_t & ub ) const {
+    sa = a.term<K,I>( sa ); sb = b.term<K,I>( sb ); ua = a.term<L,I>( ua ); ub = b.term<L,I>( ub );
+  }
+  template<int K, int L> FD_DEVM void col2( int64_t & sa, int64_t & sb, int64_t & ua, int64_t & ub ) const {
+    t2<K,L,0>( sa, sb, ua, ub ); t2<K,L,1>( sa, sb, ua, ub ); t2<K,L,2>( sa, sb, ua, ub ); t2<K,L,3>( sa, sb, ua, ub );
+    t2<K,L,4>( sa, sb, ua, ub ); t2<K,L,5>( sa, sb, ua, ub ); t2<K,L,6>( sa, sb, ua, ub ); t2<K,L,7>( sa, sb, ua, ub );
+    t2<K,L,8>( sa, sb, ua, ub ); t2<K,L,9>( sa, sb, ua, ub );
   }
 };
 
@@ -204,6 +262,20 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
   fd_fe_pre_f( f2, f );
   fd_fe_pre_g( g19, g );
   fd_fe_mul_pre( h, f, f2, g, g19 );
+}
+
+/* ha = fa*ga and hb = fb*gb, interleaved (fd_mul_cols2) */
+FD_DEV void fd_fe_mul2_pre( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int32_t const (&fa2)[10], fd_gpu_fe_t const & ga, int32_t const (&ga19)[10],
+                            fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int32_t const (&fb2)[10], fd_gpu_fe_t const & gb, int32_t const (&gb19)[10] ) {
+  fd_mul_cols2 c = { { fa.v, fa2, ga.v, ga19 }, { fb.v, fb2, gb.v, gb19 } };
+  fd_fe_chain2( ha, hb, c );
+}
+FD_DEV void fd_fe_mul2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, fd_gpu_fe_t const & ga,
+                        fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, fd_gpu_fe_t const & gb ) {
+  int32_t fa2[10], ga19[10], fb2[10], gb19[10];
+  fd_fe_pre_f( fa2, fa ); fd_fe_pre_g( ga19, ga );
+  fd_fe_pre_f( fb2, fb ); fd_fe_pre_g( gb19, gb );
+  fd_fe_mul2_pre( ha, fa, fa2, ga, ga19, hb, fb, fb2, gb, gb19 );
 }
 
 /* h = n*f^2, n in {1,2}, with the AVX SQN operand convention

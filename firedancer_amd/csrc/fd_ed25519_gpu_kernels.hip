@@ -189,9 +189,10 @@ FD_DEV uint8_t fd_op_enc( int tbl, int d ) {
   return (uint8_t)(FD_OP_ADD | (tbl << 6) | ((d < 0) << 5) | (a >> 1));
 }
 
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(256, 4)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start ) {
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
@@ -219,7 +220,7 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t 
   if( st != FD_ST_PENDING ) { op_start[i] = FD_OPS_MAX; return; }
 
   uint64_t dig[8];
-  fd_sha512_ram( dig, R, A, M, d.msg_sz );
+  fd_sha512_ram( dig, R, A, M, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
   uint64_t k[4];
   fd_sc_reduce( k, dig );
 
@@ -422,26 +423,25 @@ FD_DEV void fd_tab_lane( fe & v, int32_t const * p ) {
   v.v[8] = c.x; v.v[9] = c.y;
 }
 
+/* An add step's table entry E (the four lanes, a negative digit's lanes 1
+   and 2 swapped) for op (see fd_op_enc): the Bi table from its LDS copy,
+   the per-signature Ai table from HBM/L2. */
+FD_DEV void fd_entry_at( fe & E0, fe & E1, fe & E2, fe & E3, int32_t const * ent, int neg ) {
+  fd_tab_lane( E0, ent );
+  fd_tab_lane( E1, ent + (neg ? 2 : 1)*FD_TAB_LANE );
+  fd_tab_lane( E2, ent + (neg ? 1 : 2)*FD_TAB_LANE );
+  fd_tab_lane( E3, ent + 3*FD_TAB_LANE );
+}
+FD_DEV void fd_entry( fe & E0, fe & E1, fe & E2, fe & E3, int op, int32_t const * tab_i, int32_t const * bi ) {
+  int e = op & 7, neg = (op >> 5) & 1;
+  if( op & 0x40 ) fd_entry_at( E0, E1, E2, E3, bi    + e*FD_TAB_ENTRY, neg );
+  else            fd_entry_at( E0, E1, E2, E3, tab_i + e*FD_TAB_ENTRY, neg );
+}
+
 FD_DEV int fd_wave_min( int x ) {
 #pragma unroll
   for( int o=32; o>0; o>>=1 ) { int y = __shfl_xor( x, o, 64 ); x = y < x ? y : x; }
   return x;
-}
-
-/* p1p1 -> p3 conversion, lanes [Z, Y, X, T] = [t2*t3, t1*t2, t0*t3, t0*t1]:
-   operand for operand the reference's MUL(perm(vt,2,1,0,0),
-   perm(vt,3,2,3,1)) (avx/fd_ed25519_ge.c:506-508); its lanes Z, Y, X are
-   also the p1p1 -> p2 conversion MUL(vt, perm(vt,3,2,3,3)) (:521-522).
-   The operand pre-scales shared between the four products (19 t3, 2 t0)
-   are formed once. */
-FD_DEV void fd_conv( fe & Z, fe & Y, fe & X, fe & T, fe4 const & t ) {
-  int32_t g3[10], f0[10];
-  fd_fe_pre_g( g3, t.l[3] );
-  fd_fe_pre_f( f0, t.l[0] );
-  { int32_t f2[10]; fd_fe_pre_f( f2, t.l[2] ); fd_fe_mul_pre( Z, t.l[2], f2, t.l[3], g3 ); }
-  fd_fe_mul_pre( X, t.l[0], f0, t.l[3], g3 );
-  { int32_t f1[10], g2[10]; fd_fe_pre_f( f1, t.l[1] ); fd_fe_pre_g( g2, t.l[2] ); fd_fe_mul_pre( Y, t.l[1], f1, t.l[2], g2 ); }
-  { int32_t g1[10]; fd_fe_pre_g( g1, t.l[1] ); fd_fe_mul_pre( T, t.l[0], f0, t.l[1], g1 ); }
 }
 
 extern "C" __global__ void __launch_bounds__(256, FD_DSM_WAVES)
@@ -523,72 +523,77 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 #pragma unroll
   for( int l=0; l<4; l++ ) fd_fe_set( vt.l[l], l ? 1 : 0 );
   int32_t const * tab_i = tab + ii*FD_TAB_SIG;
+  /* the Bi table (8 cached odd multiples of B, 1.5 KiB) resident in LDS */
+  __shared__ __attribute__((aligned(16))) int32_t bi_tab[8*FD_TAB_ENTRY];
+  for( int k=threadIdx.x; k<8*FD_TAB_ENTRY; k+=blockDim.x ) bi_tab[k] = fd_gpu_bi_tab[k];
+  __syncthreads();
   int t0 = fd_wave_min( start );
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
     int op = (t >= start) ? (int)ops[(uint64_t)t*n + ii] : 0;
     int is_add = op & FD_OP_ADD;
-    int e   = op & 7;
     int neg = (op >> 5) & 1;
-    fe Z, Y, X, T; fd_conv( Z, Y, X, T, vt );
+    fe E0, E1, E2, E3;
+    /* per-lane selects as v_bfi_b32 on opaque lane masks (a boolean
+       condition lets LLVM turn groups of selects into exec-masked
+       branches) */
+    uint32_t ma = (uint32_t)fd_opaque( -(int32_t)(is_add != 0) );
 
+    /* The eight products as four interleaved pairs (fd_fe_mul2):
+         [Z, X], [Y, T]  p1p1 -> p3 conversion [Z,Y,X,T] = [t2 t3, t1 t2,
+                         t0 t3, t0 t1]: operand for operand the reference's
+                         MUL(perm(vt,2,1,0,0), perm(vt,3,2,3,1))
+                         (avx/fd_ed25519_ge.c:506-508); its Z, Y, X are also
+                         the p1p1 -> p2 conversion MUL(vt, perm(vt,3,2,3,3))
+                         (:521-522).  The pre-scales 19 t3, 2 t0 are shared.
+         [P, Q], [R, S]  the op's products */
+    fe Z, Y, X, T;
+    {
+      int32_t g3[10], f0[10];
+      fd_fe_pre_g( g3, vt.l[3] );
+      fd_fe_pre_f( f0, vt.l[0] );
+      { int32_t f2[10]; fd_fe_pre_f( f2, vt.l[2] );
+        fd_fe_mul2_pre( Z, vt.l[2], f2, vt.l[3], g3, X, vt.l[0], f0, vt.l[3], g3 ); }
+      { int32_t f1[10], g2[10], g1[10]; fd_fe_pre_f( f1, vt.l[1] ); fd_fe_pre_g( g2, vt.l[2] ); fd_fe_pre_g( g1, vt.l[1] );
+        fd_fe_mul2_pre( Y, vt.l[1], f1, vt.l[2], g2, T, vt.l[0], f0, vt.l[1], g1 ); }
+    }
     /* the table entry is read by add steps only (the Ai table does not fit
        the caches at full batch size, so D steps must not touch it) */
-    fe E0, E1, E2, E3;
-    if( is_add ) {
-      int32_t const * ent = ((op & 0x40) ? fd_gpu_bi_tab : tab_i) + e*FD_TAB_ENTRY;
-      fd_tab_lane( E0, ent );
-      fd_tab_lane( E1, ent + (neg ? 2 : 1)*FD_TAB_LANE );
-      fd_tab_lane( E2, ent + (neg ? 1 : 2)*FD_TAB_LANE );
-      fd_tab_lane( E3, ent + 3*FD_TAB_LANE );
-    }
+    if( is_add ) fd_entry( E0, E1, E2, E3, op, tab_i, bi_tab );
     fe h0, h1, h2, h3;   /* P, Q, R, S */
     {
-      fe xy, g;
+      fe xy, g0, g1;
 #pragma unroll
       for( int k=0; k<10; k++ ) {
         xy.v[k] = (int32_t)((uint32_t)X.v[k] + (uint32_t)Y.v[k]);
-        g.v[k]  = is_add ? E2.v[k] : xy.v[k];
+        g0.v[k] = (int32_t)fd_sel( ma, (uint32_t)E2.v[k], (uint32_t)xy.v[k] );
+        g1.v[k] = (int32_t)fd_sel( ma, (uint32_t)E0.v[k], 2u*(uint32_t)Z.v[k] );
       }
-      fd_fe_mul( h0, xy, g );
+      fd_fe_mul2( h0, xy, g0, h1, Z, g1 );
     }
     {
-      fe g;
-#pragma unroll
-      for( int k=0; k<10; k++ ) g.v[k] = is_add ? E0.v[k] : (int32_t)(2u*(uint32_t)Z.v[k]);
-      fd_fe_mul( h1, Z, g );
-    }
-    {
-      fe f, g;
+      fe f2, g2, f3, g3;
 #pragma unroll
       for( int k=0; k<10; k++ ) {
-        f.v[k] = is_add ? (int32_t)((uint32_t)Y.v[k] - (uint32_t)X.v[k]) : Y.v[k];
-        g.v[k] = is_add ? E1.v[k] : Y.v[k];
+        f2.v[k] = (int32_t)fd_sel( ma, (uint32_t)Y.v[k] - (uint32_t)X.v[k], (uint32_t)Y.v[k] );
+        g2.v[k] = (int32_t)fd_sel( ma, (uint32_t)E1.v[k], (uint32_t)Y.v[k] );
+        f3.v[k] = (int32_t)fd_sel( ma, (uint32_t)T.v[k],  (uint32_t)X.v[k] );
+        g3.v[k] = (int32_t)fd_sel( ma, (uint32_t)E3.v[k], (uint32_t)X.v[k] );
       }
-      fd_fe_mul( h2, f, g );
+      fd_fe_mul2( h2, f2, g2, h3, f3, g3 );
     }
-    {
-      fe f, g;
-#pragma unroll
-      for( int k=0; k<10; k++ ) {
-        f.v[k] = is_add ? T.v[k]  : X.v[k];
-        g.v[k] = is_add ? E3.v[k] : X.v[k];
-      }
-      fd_fe_mul( h3, f, g );
-    }
-    int pos = is_add && !neg;
+    uint32_t mp = (uint32_t)fd_opaque( -(int32_t)(is_add && !neg) );
 #pragma unroll
     for( int k=0; k<10; k++ ) {
       uint32_t P = h0.v[k], Q = h1.v[k], R = h2.v[k], S = h3.v[k];
-      uint32_t PR = P - R, Q2 = 2u*Q;
-      uint32_t o0 = PR - (is_add ? 0u : S);
-      uint32_t o1 = R + (is_add ? P : S);
-      uint32_t u  = is_add ? Q2 : R;            /* o2 = u - S */
-      uint32_t w  = is_add ? Q2 : Q - R;        /* o3 = w + S */
-      uint32_t o2 = u - S, o3 = w + S;
+      uint32_t Q2 = 2u*Q;
+      uint32_t o0 = P - R - (S & ~ma);
+      uint32_t o1 = R + fd_sel( ma, P, S );
+      uint32_t o2 = fd_sel( ma, Q2, R )     - S;
+      uint32_t o3 = fd_sel( ma, Q2, Q - R ) + S;
       vt.l[0].v[k] = (int32_t)o0;
       vt.l[1].v[k] = (int32_t)o1;
-      vt.l[2].v[k] = (int32_t)(pos ? o3 : o2);
-      vt.l[3].v[k] = (int32_t)(pos ? o2 : o3);
+      vt.l[2].v[k] = (int32_t)fd_sel( mp, o3, o2 );
+      vt.l[3].v[k] = (int32_t)fd_sel( mp, o2, o3 );
     }
   }
   /* final p1p1 -> p2 */
@@ -642,13 +647,14 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_sha512_batch( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
                    uint64_t * __restrict__ out, int is384 ) {
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
   uint64_t st[8];
 #pragma unroll
   for( int k=0; k<8; k++ ) st[k] = fd_gpu_sha512_iv[is384 ? 1 : 0][k];
-  fd_sha512_blocks<0>( st, NULL, NULL, blob + d.msg_off, d.msg_sz );
+  fd_sha512_blocks<0>( st, NULL, NULL, blob + d.msg_off, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
   int nw = is384 ? 6 : 8;
 #pragma unroll
   for( int k=0; k<8; k++ ) if( k < nw ) out[8*i + k] = fd_bswap64( st[k] );

@@ -99,55 +99,113 @@ __constant__ static uint64_t const fd_gpu_sha512_iv[2][8] = {
   { 0xcbbb9d5dc1059ed8ULL, 0x629a292a367cd507ULL, 0x9159015a3070dd17ULL, 0x152fecd8f70e5939ULL,
     0x67332667ffc00b31ULL, 0x8eb44a8768581511ULL, 0xdb0c2e0d64f98fa7ULL, 0x47b5481dbefa4fa4ULL } };
 
+/* LDS staging of message blocks.  Every wave owns FD_SHA_STAGE_BYTES of
+   LDS; for each 128-byte block a lane's message bytes are fetched as a
+   16-byte aligned 144-byte window with 9 global_load_lds_dwordx4 (LDS-DMA:
+   no VGPR destination, the data lands while the previous block is being
+   compressed).  The DMA writes lane l's 16 bytes of instruction c at the
+   wave-uniform base + 1024 c + 16 l, so dword q of lane l's window is at
+   stage + 1024 (q>>2) + 16 l + 4 (q&3).  Chunks at or past the message end
+   are not fetched (the batch blob is readable 16 bytes past its end, so
+   the last fetched chunk never leaves it). */
+#define FD_SHA_CHUNKS      9
+#define FD_SHA_STAGE_BYTES (FD_SHA_CHUNKS*1024)
+
+FD_DEV void fd_sha_stage( uint8_t * stage, uint8_t const * win, uint8_t const * end ) {
+#pragma unroll
+  for( int c=0; c<FD_SHA_CHUNKS; c++ )
+    if( win + 16*c < end )
+      __builtin_amdgcn_global_load_lds( (void const *)(win + 16*c), (void *)(stage + 1024*c), 16, 0, 0 );
+}
+
+/* Message words FIRST..15 of a block from its staged dwords (word i is
+   window bytes d + 8 (i - FIRST) .. +7), with the padding byte and the
+   bit count of the final block. */
+template<int FIRST, int PRE>
+FD_DEV void fd_sha_words( uint64_t (&w)[16], uint32_t const (&dw)[33], uint32_t sh, int64_t mbase, uint32_t sz,
+                          uint64_t L, bool last ) {
+#pragma unroll
+  for( int i=FIRST; i<16; i++ ) {
+    int j = i - FIRST;
+    int64_t mp = mbase + 8*i;                        /* message byte offset of this word */
+    uint64_t wv = ((uint64_t)__builtin_amdgcn_alignbit( dw[2*j+2], dw[2*j+1], sh ) << 32)
+                | __builtin_amdgcn_alignbit( dw[2*j+1], dw[2*j], sh );
+    /* rem = message bytes left at this word: >= 8 a full word, 0..7 the
+       word holding the 0x80 padding byte (at hashed offset L), < 0 zero */
+    int64_t rem = (int64_t)sz - mp;
+    uint32_t rb = (uint32_t)rem * 8u;
+    uint64_t part = ( wv & ((1ULL << (rb & 63u)) - 1ULL) ) | ( 0x80ULL << (rb & 63u) );
+    uint64_t v = rem >= 8 ? wv : ( rem >= 0 ? part : 0ULL );
+    uint64_t be = fd_bswap64( v );
+    if( last && i==15 ) be = L << 3;                 /* bit count (high word 0) */
+    w[i] = be;
+  }
+}
+
 /* SHA-512 compression over PRE || M(sz), one lane per message, where the
    PRE-byte prefix (PRE = 64: R || A of an Ed25519 signature; PRE = 0: a
-   plain message) is read from R and A.  Each 128-byte message block is
-   fetched as aligned dwords and realigned with v_alignbit (prefix words
-   never straddle: PRE is a multiple of 8).  st holds the initial state
-   on entry and the final state on return.  Streaming semantics (padding,
-   bit count) of src/ballet/sha512/fd_sha512.c:265-399. */
+   plain message) is read from R and A.  Block b's message bytes start at
+   message offset mo = (b ? 128 b - PRE : 0); they are staged through LDS
+   (above), read back as 33 dwords and realigned with v_alignbit (prefix
+   words never straddle: PRE is a multiple of 8).  stage is this wave's
+   LDS area.  st holds the initial state on entry and the final state on
+   return.  Streaming semantics (padding, bit count) of
+   src/ballet/sha512/fd_sha512.c:265-399. */
+/* Read back the 33 staged dwords of a block whose first message byte is
+   at window byte d: dword dq+4m+r of the window is at
+   stage + off[r] + 1024 m (immediate offsets). */
+FD_DEV void fd_sha_read( uint32_t (&dw)[33], uint8_t const * stage, uint32_t d ) {
+  uint32_t lane = threadIdx.x & 63u, dq = d >> 2, off[4];
+#pragma unroll
+  for( int r=0; r<4; r++ ) {
+    uint32_t q = dq + (uint32_t)r;
+    off[r] = ((q >> 2) << 10) + 16u*lane + 4u*(q & 3u);
+  }
+  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+#pragma unroll
+  for( int k=0; k<33; k++ ) dw[k] = *(uint32_t const *)( stage + off[k & 3] + 1024u*(uint32_t)(k >> 2) );
+}
+
+/* The block's words are formed (its staged dwords dead) before the next
+   block's DMA may overwrite the stage; then compression runs while the
+   DMA is in flight. */
+FD_DEV void fd_sha_next( uint64_t (&w)[16], uint8_t * stage, uint8_t const * win, uint8_t const * end, bool more ) {
+#pragma unroll
+  for( int i=0; i<16; i++ ) asm volatile( "" : "+v"(w[i]) );
+  asm volatile( "s_waitcnt lgkmcnt(0)" ::: "memory" );
+  if( more ) fd_sha_stage( stage, win, end );
+}
+
+FD_DEV uint8_t const * fd_floor16( uint8_t const * p ) { return (uint8_t const *)((uintptr_t)p & ~(uintptr_t)15); }
+
 template<int PRE>
-FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
+FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz,
+                              uint8_t * stage ) {
   uint64_t L = (uint64_t)PRE + sz;                   /* bytes hashed */
   uint32_t nblk = (uint32_t)((L + 17ULL + 127ULL) >> 7);
-  uint32_t mis = (uint32_t)((uintptr_t)M & 3u);
-  uint32_t const * mw = (uint32_t const *)(M - mis);  /* aligned view of M */
-  uint32_t sh = mis * 8u;
-  for( uint32_t b=0; b<nblk; b++ ) {
-    uint64_t w[16];
-    if( PRE && b == 0 ) {
+  uint8_t const * end = M + sz;
+  uint64_t w[16];
+  uint32_t dw[33];
+  /* block 0: PRE prefix bytes, then message bytes 0 .. 127-PRE */
+  fd_sha_stage( stage, fd_floor16( M ), end );
+  if( PRE ) {
 #pragma unroll
-      for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
+    for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
 #pragma unroll
-      for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
-    }
-    /* message dwords covering this block's message bytes */
-    int first = b == 0 ? PRE/8 : 0;
-    int64_t mbase = (int64_t)b*128 - PRE;            /* message offset of word 0 of this block */
-#pragma unroll
-    for( int i=0; i<16; i++ ) {
-      if( i < first ) continue;
-      int64_t mp = mbase + 8*i;                      /* message byte offset of this word */
-      uint64_t v = 0;
-      if( mp + 8 <= (int64_t)sz ) {
-        uint32_t const * q = mw + (mp >> 2);
-        uint32_t q0 = q[0], q1 = q[1], q2 = q[2];
-        v = ((uint64_t)__builtin_amdgcn_alignbit( q2, q1, sh ) << 32) | __builtin_amdgcn_alignbit( q1, q0, sh );
-      } else {
-        if( mp < (int64_t)sz ) {
-          uint64_t keep = (uint64_t)((int64_t)sz - mp);  /* 1..7 bytes */
-          uint32_t const * q = mw + (mp >> 2);
-          uint32_t q0 = q[0], q1 = q[1], q2 = q[2];
-          v = ((uint64_t)__builtin_amdgcn_alignbit( q2, q1, sh ) << 32) | __builtin_amdgcn_alignbit( q1, q0, sh );
-          v &= (1ULL << (8*keep)) - 1ULL;
-        }
-        uint64_t pos = (uint64_t)(mp + PRE);
-        if( pos <= L && L < pos + 8 ) v |= 0x80ULL << (8*(L-pos));
-      }
-      uint64_t be = fd_bswap64( v );
-      if( b==nblk-1 && i==15 ) be = L << 3;          /* bit count (high word 0) */
-      w[i] = be;
-    }
+    for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
+  }
+  uint32_t d = (uint32_t)((uintptr_t)M & 15u);
+  fd_sha_read( dw, stage, d );
+  fd_sha_words<PRE/8, PRE>( w, dw, (d & 3u) * 8u, -PRE, sz, L, nblk == 1 );
+  fd_sha_next( w, stage, fd_floor16( M + 128 - PRE ), end, nblk > 1 );
+  fd_sha512_compress( st, w );
+  /* block b >= 1: message bytes 128 b - PRE .. +127 */
+  for( uint32_t b=1; b<nblk; b++ ) {
+    int64_t mbase = (int64_t)b*128 - PRE;
+    d = (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 15u);
+    fd_sha_read( dw, stage, d );
+    fd_sha_words<0, PRE>( w, dw, (d & 3u) * 8u, mbase, sz, L, b == nblk-1 );
+    fd_sha_next( w, stage, fd_floor16( M + mbase + 128 ), end, b + 1 < nblk );
     fd_sha512_compress( st, w );
   }
 }
@@ -155,11 +213,12 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
 /* SHA-512 of R(32) || A(32) || M(sz) (fd_ed25519_user.c:411-414).
    Returns the digest as 8 words where word i holds digest bytes
    8i..8i+7 little endian. */
-FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz ) {
+FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz,
+                          uint8_t * stage ) {
   uint64_t st[8];
 #pragma unroll
   for( int i=0; i<8; i++ ) st[i] = fd_gpu_sha512_iv[0][i];
-  fd_sha512_blocks<64>( st, R, A, M, sz );
+  fd_sha512_blocks<64>( st, R, A, M, sz, stage );
 #pragma unroll
   for( int i=0; i<8; i++ ) dig[i] = fd_bswap64( st[i] );
 }
