@@ -103,91 +103,7 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
   for( int i=0; i<8; i++ ) w[i] = fd_ld_u32_unaligned( p + 4*i );
 }
 
-/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) is, for scalars below
-   2^253 (k < L; S < L once the S check passed), exactly the width-5
-   signed window recoding: at each set bit i take w = bits i..i+4; the
-   digit is w (w < 16) or w - 32 (w >= 16; the reference's subtract at
-   b=4 whose carry loop adds 2^(i+5)), bits i..i+4 are cleared, and bits
-   i+5, i+6 are only inspected (b=5,6 always break or continue).  No
-   carry ever passes bit 255.  So digits are found by counting trailing
-   zeros instead of walking all 256 positions.  tests/test_oracle.py
-   (slide properties) and the GPU parity suite pin this against the
-   reference's digit-by-digit loop. */
-
-struct fd_u256 { uint64_t w[4]; };
-
-FD_DEV uint64_t fd_u256_get( fd_u256 const & v, int j ) {
-  uint64_t r = v.w[0];
-  r = j == 1 ? v.w[1] : r;
-  r = j == 2 ? v.w[2] : r;
-  r = j == 3 ? v.w[3] : r;
-  return j > 3 ? 0ULL : r;
-}
-
-FD_DEV void fd_u256_setbit( fd_u256 & v, int b ) {
-  uint64_t bit = 1ULL << (b & 63);
-#pragma unroll
-  for( int j=0; j<4; j++ ) v.w[j] |= (b >> 6) == j ? bit : 0ULL;
-}
-
-FD_DEV int fd_u256_nz( fd_u256 const & v ) { return (v.w[0] | v.w[1] | v.w[2] | v.w[3]) != 0; }
-
-FD_DEV int fd_u256_ctz( fd_u256 const & v ) {
-  int r = 192 + (int)__builtin_ctzll( v.w[3] | (1ULL<<63) );
-  r = v.w[2] ? 128 + (int)__builtin_ctzll( v.w[2] ) : r;
-  r = v.w[1] ?  64 + (int)__builtin_ctzll( v.w[1] ) : r;
-  r = v.w[0] ?       (int)__builtin_ctzll( v.w[0] ) : r;
-  return r;
-}
-
-/* number of set bits of m strictly below bit i (0 <= i < 256) */
-FD_DEV int fd_u256_rank( fd_u256 const & m, int i ) {
-  int wd = i >> 6, sh = i & 63;
-  int c = 0;
-#pragma unroll
-  for( int j=0; j<4; j++ ) {
-    uint64_t x = m.w[j];
-    uint64_t mask = j < wd ? ~0ULL : (j == wd ? ((1ULL << sh) - 1ULL) : 0ULL);
-    c += __builtin_popcountll( x & mask );
-  }
-  return c;
-}
-
-/* one wNAF-5 digit: returns position i and digit d, updates v */
-FD_DEV void fd_wnaf_next( fd_u256 & v, int & i, int & d ) {
-  i = fd_u256_ctz( v );
-  int wd = i >> 6, sh = i & 63;
-  uint64_t lo = fd_u256_get( v, wd ), hi = fd_u256_get( v, wd+1 );
-  uint32_t win = (uint32_t)(((lo >> sh) | (sh > 59 ? hi << (64-sh) : 0ULL)) & 31ULL);
-  d = win < 16u ? (int)win : (int)win - 32;
-  /* clear bits i..i+4 */
-  uint64_t clo = (uint64_t)win << sh;
-  uint64_t chi = sh > 59 ? ((uint64_t)win >> (64-sh)) : 0ULL;
-  /* for a negative digit add 2^(i+5) */
-  int p = i + 5, pw = p >> 6;
-  uint64_t add = d < 0 ? (1ULL << (p & 63)) : 0ULL;
-  uint64_t carry = 0;
-#pragma unroll
-  for( int j=0; j<4; j++ ) {
-    uint64_t x = v.w[j];
-    x ^= j == wd ? clo : 0ULL;
-    x ^= j == wd+1 ? chi : 0ULL;
-    uint64_t a = (j == pw ? add : 0ULL) + carry;
-    uint64_t y = x + a;
-    carry = y < x ? 1ULL : 0ULL;
-    v.w[j] = y;
-  }
-}
-
-/* Op encoding of the DSM's per-lane op stream (see fd_k_dsm):
-     0x00                      D: doubling step
-     0x80 | t<<6 | neg<<5 | e  A: add (t=0: Ai table of -A, t=1: Bi table),
-                                  digit = (neg ? -1 : 1) * (2e+1) */
-#define FD_OP_ADD 0x80
-FD_DEV uint8_t fd_op_enc( int tbl, int d ) {
-  int a = d < 0 ? -d : d;
-  return (uint8_t)(FD_OP_ADD | (tbl << 6) | ((d < 0) << 5) | (a >> 1));
-}
+#include "fd_ed25519_gpu_wnaf.h"
 
 extern "C" __global__ void __launch_bounds__(256, 4)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
@@ -224,49 +140,11 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t 
   uint64_t k[4];
   fd_sc_reduce( k, dig );
 
-  /* Recode k and S and write the DSM op stream.  The stream runs from
-     bit 255 down to 0; for each bit: D, then an add for k's digit, then
-     one for S's (avx/fd_ed25519_ge.c:490-523).  Streams are right-aligned
-     at FD_OPS_MAX (every lane of a wave then finishes on the same step)
-     and laid out back to front: the ops of bits < b occupy the last
-     b + (adds at bits < b) slots.  D is byte 0 and the buffer is zeroed
-     before this kernel, so only adds are stored; the DSM reads the gap
-     before op_start as D, an exact no-op on the identity. */
-  fd_u256 Vk = { { k[0], k[1], k[2], k[3] } };
-  fd_u256 Vs = { { ((uint64_t)sw[1]<<32)|sw[0], ((uint64_t)sw[3]<<32)|sw[2],
-                   ((uint64_t)sw[5]<<32)|sw[4], ((uint64_t)sw[7]<<32)|sw[6] } };
-  fd_u256 Ms = { { 0, 0, 0, 0 } }, Mk = { { 0, 0, 0, 0 } };
-  int ns = 0, nk = 0;
-  {
-    fd_u256 v = Vs;
-    while( fd_u256_nz( v ) ) {
-      int b, dg; fd_wnaf_next( v, b, dg );
-      fd_u256_setbit( Ms, b );
-      ns++;
-    }
-  }
-  {
-    fd_u256 v = Vk;
-    while( fd_u256_nz( v ) ) {
-      int b, dg; fd_wnaf_next( v, b, dg );
-      int s_at = (int)((fd_u256_get( Ms, b>>6 ) >> (b & 63)) & 1ULL);
-      int pos  = FD_OPS_MAX - 1 - ( b + nk + fd_u256_rank( Ms, b ) ) - s_at;
-      ops[(uint64_t)pos*n + i] = fd_op_enc( 0, dg );
-      fd_u256_setbit( Mk, b );
-      nk++;
-    }
-  }
-  {
-    fd_u256 v = Vs;
-    int cs = 0;
-    while( fd_u256_nz( v ) ) {
-      int b, dg; fd_wnaf_next( v, b, dg );
-      int pos = FD_OPS_MAX - 1 - ( b + cs + fd_u256_rank( Mk, b ) );
-      ops[(uint64_t)pos*n + i] = fd_op_enc( 1, dg );
-      cs++;
-    }
-  }
-  op_start[i] = FD_OPS_MAX - 256 - nk - ns;
+  /* recode k and S into the op stream (fd_ed25519_gpu_wnaf.h) */
+  uint32_t kw[8];
+#pragma unroll
+  for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
+  op_start[i] = fd_recode( sw, kw, ops + i, n );
 }
 
 /* ------------------------------------------------------------------ */

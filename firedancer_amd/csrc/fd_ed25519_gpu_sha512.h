@@ -62,6 +62,9 @@ FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
   return ((uint64_t)__builtin_amdgcn_alignbit( w2, w1, mis * 8u ) << 32) | __builtin_amdgcn_alignbit( w1, w0, mis * 8u );
 }
 
+#ifndef FD_SHA_UNROLL
+#define FD_SHA_UNROLL 0
+#endif
 #define FD_SHA_ROUND(j,kt) do {                                                   \
     uint64_t S1 = fd_rotr64(e,14) ^ fd_rotr64(e,18) ^ fd_rotr64(e,41);          \
     uint64_t ch = (e&f) ^ (~e&g);                                               \
@@ -77,7 +80,11 @@ FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
   uint64_t a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
 #pragma unroll
   for( int j=0; j<16; j++ ) FD_SHA_ROUND( j, fd_gpu_sha512_k[j] );
+#if FD_SHA_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for( int r=16; r<80; r+=16 ) {
 #pragma unroll
     for( int j=0; j<16; j++ ) {

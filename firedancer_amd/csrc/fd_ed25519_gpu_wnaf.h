@@ -1,0 +1,121 @@
+/* fd_ed25519_gpu_wnaf.h -- scalar recoding of the DSM op stream
+   (device, and host for tests/test_recode_host.py).
+
+   fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) is, for scalars below
+   2^253 (k < L; S < L once the S check passed), exactly the width-5
+   signed window recoding: at each set bit i take w = bits i..i+4; the
+   digit is w (w < 16) or w - 32 (w >= 16; the reference's subtract at
+   b=4 whose carry loop adds 2^(i+5)), bits i..i+4 are cleared, and bits
+   i+5, i+6 are only inspected (b=5,6 always break or continue).  No
+   carry ever passes bit 255.  So digits are found by counting trailing
+   zeros instead of walking all 256 positions. */
+#ifndef FD_ED25519_GPU_WNAF_H
+#define FD_ED25519_GPU_WNAF_H
+#include "fd_ed25519_gpu_fe.h"
+#include "fd_ed25519_gpu_private.h"
+
+FD_DEV uint32_t fd_alignbit( uint32_t hi, uint32_t lo, uint32_t t ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit( hi, lo, t );
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (t & 31u));
+#endif
+}
+
+/* Op encoding of the DSM's per-lane op stream (see fd_k_dsm):
+     0x00                      D: doubling step
+     0x80 | t<<6 | neg<<5 | e  A: add (t=0: Ai table of -A, t=1: Bi table),
+                                  digit = (neg ? -1 : 1) * (2e+1) */
+#define FD_OP_ADD 0x80
+FD_DEV uint8_t fd_op_enc( int tbl, int d ) {
+  int a = d < 0 ? -d : d;
+  return (uint8_t)(FD_OP_ADD | (tbl << 6) | ((d < 0) << 5) | (a >> 1));
+}
+
+/* A scalar being recoded, as a 256-bit shift register of 8 dwords kept
+   normalized: bit 0 of d[0] is the lowest set bit, which sits at scalar
+   bit position pos (pos = FD_WN_DONE once nothing is left).  All
+   indexing is static (a per-lane word index would put the scalar in
+   scratch memory). */
+#define FD_WN_DONE 0x7fff
+struct fd_wn { uint32_t d[8]; int pos; };
+
+FD_DEV int fd_wn_nz( fd_wn const & v ) {
+  return (v.d[0] | v.d[1] | v.d[2] | v.d[3] | v.d[4] | v.d[5] | v.d[6] | v.d[7]) != 0u;
+}
+
+/* shift right until bit 0 is set (whole dwords first: only for runs of
+   >= 32 zero bits) */
+FD_DEV void fd_wn_norm( fd_wn & v ) {
+  if( !fd_wn_nz( v ) ) { v.pos = FD_WN_DONE; return; }
+  while( v.d[0] == 0u ) {
+#pragma unroll
+    for( int j=0; j<7; j++ ) v.d[j] = v.d[j+1];
+    v.d[7] = 0u;
+    v.pos += 32;
+  }
+  uint32_t t = (uint32_t)__builtin_ctz( v.d[0] );
+#pragma unroll
+  for( int j=0; j<7; j++ ) v.d[j] = fd_alignbit( v.d[j+1], v.d[j], t );
+  v.d[7] >>= t;
+  v.pos += (int)t;
+}
+
+FD_DEV void fd_wn_init( fd_wn & v, uint32_t const (&w)[8] ) {
+#pragma unroll
+  for( int j=0; j<8; j++ ) v.d[j] = w[j];
+  v.pos = 0;
+  fd_wn_norm( v );
+}
+
+/* one wNAF-5 digit at bit v.pos: w = bits pos..pos+4, digit w or w - 32;
+   the register loses the digit (a negative one adds 2^(pos+5)) and is
+   renormalized */
+FD_DEV int fd_wn_step( fd_wn & v ) {
+  uint32_t win = v.d[0] & 31u;
+  int neg = win >= 16u;
+  /* bits 0..4 hold win, so subtracting it never borrows; a negative digit
+     then adds 2^5 (carry propagated) */
+  uint64_t c = (uint64_t)(v.d[0] - win) + (neg ? 32u : 0u);
+  v.d[0] = (uint32_t)c;
+#pragma unroll
+  for( int j=1; j<8; j++ ) { c = (uint64_t)v.d[j] + (c >> 32); v.d[j] = (uint32_t)c; }
+  fd_wn_norm( v );
+  return neg ? (int)win - 32 : (int)win;
+}
+
+
+/* Recode S (sw) and k (kw) and write the DSM op stream of one signature
+   (byte t at ops[t*stride], zero-filled by the caller); returns op_start.
+   The stream runs from bit 255 down to 0; for each bit: D, then an add
+   for k's digit, then one for S's (avx/fd_ed25519_ge.c:490-523).  Streams
+   are right-aligned at FD_OPS_MAX (every lane of a wave then finishes on
+   the same step) and laid out back to front: the ops of bits < b occupy
+   the last b + (adds at bits < b) slots.  D is byte 0, so only adds are
+   stored; the DSM reads the gap before op_start as D, an exact no-op on
+   the identity. */
+FD_DEV int fd_recode( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t * ops, uint64_t stride ) {
+  /* Both scalars are recoded in one pass, digits merged in ascending bit
+     order: with cnt adds already placed (all at lower bits, or S's at
+     the same bit), a digit at bit b goes to FD_OPS_MAX-1-(b+cnt).  At a
+     shared bit S's digit is placed first (it is the later op). */
+  fd_wn vs, vk;
+  fd_wn_init( vs, sw );
+  fd_wn_init( vk, kw );
+  int cnt = 0;
+  /* scalars below 2^253 have every digit at bit <= 253 and at most 2 x 127
+     of them; the bounds only keep a corrupted state inside the buffer */
+  while( (vs.pos != FD_WN_DONE || vk.pos != FD_WN_DONE) && cnt < 2*128 ) {
+    int take_s = vs.pos <= vk.pos;
+    fd_wn v = take_s ? vs : vk;
+    int b  = v.pos;
+    if( b > 255 ) break;
+    int dg = fd_wn_step( v );
+    ops[(uint64_t)(FD_OPS_MAX - 1 - (b + cnt))*stride] = fd_op_enc( take_s, dg );
+    cnt++;
+    if( take_s ) vs = v; else vk = v;
+  }
+  return FD_OPS_MAX - 256 - cnt;
+}
+
+#endif /* FD_ED25519_GPU_WNAF_H */
