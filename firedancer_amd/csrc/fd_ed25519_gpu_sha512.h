@@ -62,15 +62,46 @@ FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
   return ((uint64_t)__builtin_amdgcn_alignbit( w2, w1, mis * 8u ) << 32) | __builtin_amdgcn_alignbit( w1, w0, mis * 8u );
 }
 
+#ifndef FD_SHA_B3
+#define FD_SHA_B3 1
+#endif
+/* 3-input bitwise ops as one v_bitop3_b32 per 32-bit half (gfx950):
+   truth tables 0x96 (x^y^z) and 0xE8 (majority), both symmetric in their
+   inputs, so independent of the operand-order convention. */
+FD_DEV uint32_t fd_bitop3_96( uint32_t x, uint32_t y, uint32_t z ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32( x, y, z, 0x96 );
+#else
+  return x ^ y ^ z;
+#endif
+}
+FD_DEV uint32_t fd_bitop3_e8( uint32_t x, uint32_t y, uint32_t z ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32( x, y, z, 0xE8 );
+#else
+  return (x & y) | (x & z) | (y & z);
+#endif
+}
+FD_DEV uint64_t fd_xor3_64( uint64_t x, uint64_t y, uint64_t z ) {
+  if( !FD_SHA_B3 ) return x ^ y ^ z;
+  return ((uint64_t)fd_bitop3_96( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
+       | fd_bitop3_96( (uint32_t)x, (uint32_t)y, (uint32_t)z );
+}
+FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
+  if( !FD_SHA_B3 ) return (x&y) ^ (x&z) ^ (y&z);
+  return ((uint64_t)fd_bitop3_e8( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
+       | fd_bitop3_e8( (uint32_t)x, (uint32_t)y, (uint32_t)z );
+}
+
 #ifndef FD_SHA_UNROLL
 #define FD_SHA_UNROLL 0
 #endif
 #define FD_SHA_ROUND(j,kt) do {                                                   \
-    uint64_t S1 = fd_rotr64(e,14) ^ fd_rotr64(e,18) ^ fd_rotr64(e,41);          \
+    uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
     uint64_t ch = (e&f) ^ (~e&g);                                               \
     uint64_t t1 = h + S1 + ch + (kt) + w[j];                                    \
-    uint64_t S0 = fd_rotr64(a,28) ^ fd_rotr64(a,34) ^ fd_rotr64(a,39);          \
-    uint64_t mj = (a&b) ^ (a&c) ^ (b&c);                                        \
+    uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
+    uint64_t mj = fd_maj64( a, b, c );                                          \
     h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;                           \
   } while(0)
 
@@ -89,8 +120,8 @@ FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
 #pragma unroll
     for( int j=0; j<16; j++ ) {
       uint64_t w15 = w[(j+1)&15], w2 = w[(j+14)&15];
-      uint64_t s0 = fd_rotr64(w15,1) ^ fd_rotr64(w15,8) ^ fd_shr64(w15,7);
-      uint64_t s1 = fd_rotr64(w2,19) ^ fd_rotr64(w2,61) ^ fd_shr64(w2,6);
+      uint64_t s0 = fd_xor3_64( fd_rotr64(w15,1), fd_rotr64(w15,8), fd_shr64(w15,7) );
+      uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
       w[j] = w[j] + s0 + w[(j+9)&15] + s1;
       FD_SHA_ROUND( j, fd_gpu_sha512_k[r+j] );
     }
