@@ -137,23 +137,41 @@ FD_DEV void fd_fe_limbs( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, 
 /* COL provides template<int K> int64_t col(int64_t init) const: init +
    column K's products (a compile-time column index keeps every operand
    array access static, so nothing is demoted to scratch or LDS). */
+/* Columns K1, K2, K3 of one product with their multiply chains
+   interleaved term by term (a column of fewer terms drops out): every
+   v_mad_i64_i32 then sits at least two instructions after the MAC whose
+   accumulator it reads, so no hazard wait states (K3 < 0: two columns). */
+template<typename COL, int K1, int K2, int K3, int I>
+FD_DEV void fd_cols_step( COL const & c, int64_t & s1, int64_t & s2, int64_t & s3 ) {
+  if constexpr( I < COL::template len<K1>() ) s1 = c.template term<K1,I>( s1 );
+  if constexpr( I < COL::template len<K2>() ) s2 = c.template term<K2,I>( s2 );
+  if constexpr( K3 >= 0 ) { if constexpr( I < COL::template len<K3 < 0 ? 0 : K3>() ) s3 = c.template term<K3 < 0 ? 0 : K3,I>( s3 ); }
+}
+template<typename COL, int K1, int K2, int K3>
+FD_DEV void fd_cols( COL const & c, int64_t & s1, int64_t & s2, int64_t & s3 ) {
+  fd_cols_step<COL,K1,K2,K3,0>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,1>( c, s1, s2, s3 );
+  fd_cols_step<COL,K1,K2,K3,2>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,3>( c, s1, s2, s3 );
+  fd_cols_step<COL,K1,K2,K3,4>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,5>( c, s1, s2, s3 );
+  fd_cols_step<COL,K1,K2,K3,6>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,7>( c, s1, s2, s3 );
+  fd_cols_step<COL,K1,K2,K3,8>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,9>( c, s1, s2, s3 );
+}
+
 template<typename COL>
 FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
-  /* the even columns wait for no carry: five independent chains first */
-  int64_t S0 = c.template col<0>( FD_KEVEN );
-  int64_t S4 = c.template col<4>( FD_KEVEN );
-  int64_t S2 = c.template col<2>( FD_KEVEN );
-  int64_t S6 = c.template col<6>( FD_KEVEN );
-  int64_t S8 = c.template col<8>( FD_KEVEN );
-  int64_t c0 = S0 >> 26,                  c4 = S4 >> 26;
-  int64_t S1 = c.template col<1>( c0 ),   S5 = c.template col<5>( c4 );
-  int64_t c1 = S1 >> 25,                  c5 = S5 >> 25;
-  S2 += c1;                               S6 += c5;
-  int64_t c2 = S2 >> 26,                  c6 = S6 >> 26;
-  int64_t S3 = c.template col<3>( c2 ),   S7 = c.template col<7>( c6 );
+  /* groups in carry order: {0,4,2} and {6,8} wait for no carry, 1 needs
+     c0; {5,3} need c4 and c2 (after c1); 7 needs c6 (after c5); 9 needs
+     c8 (after c7) */
+  int64_t S0 = FD_KEVEN, S4 = FD_KEVEN, S2 = FD_KEVEN;
+  fd_cols<COL,0,4,2>( c, S0, S4, S2 );
+  int64_t S6 = FD_KEVEN, S8 = FD_KEVEN, S1 = S0 >> 26;
+  fd_cols<COL,6,8,1>( c, S6, S8, S1 );
+  S2 += S1 >> 25;
+  int64_t S5 = S4 >> 26, S3 = S2 >> 26, unused = 0;
+  fd_cols<COL,5,3,-1>( c, S5, S3, unused );
+  S6 += S5 >> 25;
+  int64_t S7 = c.template col<7>( S6 >> 26 );
   S8 += S7 >> 25;
-  int64_t c8 = S8 >> 26;
-  int64_t S9 = c.template col<9>( c8 );
+  int64_t S9 = c.template col<9>( S8 >> 26 );
   fd_fe_limbs( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
 }
 
@@ -185,6 +203,7 @@ FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, COL2 const & c ) {
    592-677: 2f, 19f, 38f). */
 struct fd_mul_cols {
   int32_t const * f; int32_t const * f2; int32_t const * g; int32_t const * g19;
+  template<int K> static constexpr int len() { return 10; }
   template<int K, int I> FD_DEVM int64_t term( int64_t acc ) const {
     int const j = K - I < 0 ? K - I + 10 : K - I;
     return fd_mad( ((I&1)&(j&1)) ? f2[I] : f[I], K - I < 0 ? g19[j] : g[j], acc );
@@ -221,19 +240,32 @@ struct fd_mul_cols2 {
   }
 };
 
+/* SQN(1) column K, term I: (operand array, limb) x (operand array, limb),
+   arrays 0 = F, 1 = 2F, 2 = 19F, 3 = 38F; FD_SQ_LEN(K) terms. */
+#define FD_SQ_LEN(K) ((K)&1 ? 5 : 6)
+__host__ __device__ constexpr unsigned char fd_sq_tab[10][6][4] = {
+  { {0,0,0,0}, {1,1,3,9}, {1,2,2,8}, {1,3,3,7}, {1,4,2,6}, {0,5,3,5} },
+  { {1,0,0,1}, {0,2,3,9}, {1,3,2,8}, {0,4,3,7}, {1,5,2,6}, {0,0,0,0} },
+  { {1,0,0,2}, {1,1,0,1}, {1,3,3,9}, {1,4,2,8}, {1,5,3,7}, {0,6,2,6} },
+  { {1,0,0,3}, {1,1,0,2}, {0,4,3,9}, {1,5,2,8}, {0,6,3,7}, {0,0,0,0} },
+  { {1,0,0,4}, {1,1,1,3}, {0,2,0,2}, {1,5,3,9}, {1,6,2,8}, {0,7,3,7} },
+  { {1,0,0,5}, {1,1,0,4}, {1,2,0,3}, {0,6,3,9}, {1,7,2,8}, {0,0,0,0} },
+  { {1,0,0,6}, {1,1,1,5}, {1,2,0,4}, {1,3,0,3}, {1,7,3,9}, {0,8,2,8} },
+  { {1,0,0,7}, {1,1,0,6}, {1,2,0,5}, {1,3,0,4}, {0,8,3,9}, {0,0,0,0} },
+  { {1,0,0,8}, {1,1,1,7}, {1,2,0,6}, {1,3,1,5}, {0,4,0,4}, {0,9,3,9} },
+  { {1,0,0,9}, {1,1,0,8}, {1,2,0,7}, {1,3,0,6}, {1,4,0,5}, {0,0,0,0} } };
+
 struct fd_sq_cols {
   int32_t const * F; int32_t const * F2; int32_t const * F19; int32_t const * F38;
+  template<int K> static constexpr int len() { return FD_SQ_LEN(K); }
+  FD_DEVM int32_t const * arr( int w ) const { return w==0 ? F : w==1 ? F2 : w==2 ? F19 : F38; }
+  template<int K, int I> FD_DEVM int64_t term( int64_t acc ) const {
+    constexpr int wa = fd_sq_tab[K][I][0], ia = fd_sq_tab[K][I][1], wb = fd_sq_tab[K][I][2], ib = fd_sq_tab[K][I][3];
+    return fd_mad( arr( wa )[ia], arr( wb )[ib], acc );
+  }
   template<int K> FD_DEVM int64_t col( int64_t a ) const {
-    if( K==0 ) { a=fd_mad(F[0],F[0],a);  a=fd_mad(F2[1],F38[9],a); a=fd_mad(F2[2],F19[8],a); a=fd_mad(F2[3],F38[7],a); a=fd_mad(F2[4],F19[6],a); a=fd_mad(F[5],F38[5],a); }
-    if( K==1 ) { a=fd_mad(F2[0],F[1],a); a=fd_mad(F[2],F38[9],a);  a=fd_mad(F2[3],F19[8],a); a=fd_mad(F[4],F38[7],a);  a=fd_mad(F2[5],F19[6],a); }
-    if( K==2 ) { a=fd_mad(F2[0],F[2],a); a=fd_mad(F2[1],F[1],a);   a=fd_mad(F2[3],F38[9],a); a=fd_mad(F2[4],F19[8],a); a=fd_mad(F2[5],F38[7],a); a=fd_mad(F[6],F19[6],a); }
-    if( K==3 ) { a=fd_mad(F2[0],F[3],a); a=fd_mad(F2[1],F[2],a);   a=fd_mad(F[4],F38[9],a);  a=fd_mad(F2[5],F19[8],a); a=fd_mad(F[6],F38[7],a); }
-    if( K==4 ) { a=fd_mad(F2[0],F[4],a); a=fd_mad(F2[1],F2[3],a);  a=fd_mad(F[2],F[2],a);    a=fd_mad(F2[5],F38[9],a); a=fd_mad(F2[6],F19[8],a); a=fd_mad(F[7],F38[7],a); }
-    if( K==5 ) { a=fd_mad(F2[0],F[5],a); a=fd_mad(F2[1],F[4],a);   a=fd_mad(F2[2],F[3],a);   a=fd_mad(F[6],F38[9],a);  a=fd_mad(F2[7],F19[8],a); }
-    if( K==6 ) { a=fd_mad(F2[0],F[6],a); a=fd_mad(F2[1],F2[5],a);  a=fd_mad(F2[2],F[4],a);   a=fd_mad(F2[3],F[3],a);   a=fd_mad(F2[7],F38[9],a); a=fd_mad(F[8],F19[8],a); }
-    if( K==7 ) { a=fd_mad(F2[0],F[7],a); a=fd_mad(F2[1],F[6],a);   a=fd_mad(F2[2],F[5],a);   a=fd_mad(F2[3],F[4],a);   a=fd_mad(F[8],F38[9],a); }
-    if( K==8 ) { a=fd_mad(F2[0],F[8],a); a=fd_mad(F2[1],F2[7],a);  a=fd_mad(F2[2],F[6],a);   a=fd_mad(F2[3],F2[5],a);  a=fd_mad(F[4],F[4],a);    a=fd_mad(F[9],F38[9],a); }
-    if( K==9 ) { a=fd_mad(F2[0],F[9],a); a=fd_mad(F2[1],F[8],a);   a=fd_mad(F2[2],F[7],a);   a=fd_mad(F2[3],F[6],a);   a=fd_mad(F2[4],F[5],a); }
+    a = term<K,0>( a ); a = term<K,1>( a ); a = term<K,2>( a ); a = term<K,3>( a ); a = term<K,4>( a );
+    if constexpr( FD_SQ_LEN(K) == 6 ) a = term<K,5>( a );
     return a;
   }
 };
