@@ -140,6 +140,10 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_set_mode.restype = ip
         L.fd_ed25519_gpu_mode.argtypes = [vp]
         L.fd_ed25519_gpu_mode.restype = ip
+        L.fd_ed25519_gpu_set_dsm_pool_min.argtypes = [vp, ul]
+        L.fd_ed25519_gpu_set_dsm_pool_min.restype = ip
+        L.fd_ed25519_gpu_dsm_pool_min.argtypes = [vp]
+        L.fd_ed25519_gpu_dsm_pool_min.restype = ul
         L.fd_ed25519_gpu_multi_new.argtypes = [vp, ip, ul, ul]
         L.fd_ed25519_gpu_multi_new.restype = vp
         L.fd_ed25519_gpu_multi_delete.argtypes = [vp]
@@ -271,6 +275,16 @@ class Engine:
     def mode(self, m: int) -> None:
         if lib().fd_ed25519_gpu_set_mode(self._h, m):
             raise EngineError(f"bad mode {m}")
+
+    @property
+    def dsm_pool_min(self) -> int:
+        """batches of at least this many signatures take the pooled DSM"""
+        return lib().fd_ed25519_gpu_dsm_pool_min(self._h)
+
+    @dsm_pool_min.setter
+    def dsm_pool_min(self, n: int) -> None:
+        if lib().fd_ed25519_gpu_set_dsm_pool_min(self._h, n):
+            raise EngineError("set_dsm_pool_min")
 
     @property
     def depth(self) -> int:

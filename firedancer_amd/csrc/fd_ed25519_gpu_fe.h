@@ -175,27 +175,90 @@ FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
   fd_fe_limbs( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
 }
 
-/* fd_fe_chain for two independent products (fd_mul_cols2), carries and
-   limb recovery as above, the column chains of the two interleaved. */
-template<typename COL2>
-FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, COL2 const & c ) {
+/* Columns K1, K2 of two independent products A and B, the four multiply
+   chains interleaved term by term (columns of fewer terms drop out). */
+template<typename CA, typename CB, int K1, int K2, int I>
+FD_DEV void fd_cols_ab_step( CA const & ca, CB const & cb, int64_t & a1, int64_t & b1, int64_t & a2, int64_t & b2 ) {
+  if constexpr( I < CA::template len<K1>() ) a1 = ca.template term<K1,I>( a1 );
+  if constexpr( I < CB::template len<K1>() ) b1 = cb.template term<K1,I>( b1 );
+  if constexpr( K2 >= 0 ) {
+    constexpr int K = K2 < 0 ? 0 : K2;
+    if constexpr( I < CA::template len<K>() ) a2 = ca.template term<K,I>( a2 );
+    if constexpr( I < CB::template len<K>() ) b2 = cb.template term<K,I>( b2 );
+  }
+}
+template<typename CA, typename CB, int K1, int K2>
+FD_DEV void fd_cols_ab( CA const & ca, CB const & cb, int64_t & a1, int64_t & b1, int64_t & a2, int64_t & b2 ) {
+  fd_cols_ab_step<CA,CB,K1,K2,0>( ca, cb, a1, b1, a2, b2 ); fd_cols_ab_step<CA,CB,K1,K2,1>( ca, cb, a1, b1, a2, b2 );
+  fd_cols_ab_step<CA,CB,K1,K2,2>( ca, cb, a1, b1, a2, b2 ); fd_cols_ab_step<CA,CB,K1,K2,3>( ca, cb, a1, b1, a2, b2 );
+  fd_cols_ab_step<CA,CB,K1,K2,4>( ca, cb, a1, b1, a2, b2 ); fd_cols_ab_step<CA,CB,K1,K2,5>( ca, cb, a1, b1, a2, b2 );
+  fd_cols_ab_step<CA,CB,K1,K2,6>( ca, cb, a1, b1, a2, b2 ); fd_cols_ab_step<CA,CB,K1,K2,7>( ca, cb, a1, b1, a2, b2 );
+  fd_cols_ab_step<CA,CB,K1,K2,8>( ca, cb, a1, b1, a2, b2 ); fd_cols_ab_step<CA,CB,K1,K2,9>( ca, cb, a1, b1, a2, b2 );
+}
+
+/* fd_fe_chain for two independent products (any column functors), carries
+   and limb recovery as above, the column chains of the two interleaved:
+   two columns of each product run together where the carry order allows
+   (four chains, every MAC three instructions after the one it depends
+   on); 7 and 9 run as two chains. */
+template<typename CA, typename CB>
+FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, CA const & ca, CB const & cb ) {
   int64_t a0 = FD_KEVEN, b0 = FD_KEVEN, a4 = FD_KEVEN, b4 = FD_KEVEN;
-  c.template col2<0,4>( a0, b0, a4, b4 );
+  fd_cols_ab<CA,CB,0,4>( ca, cb, a0, b0, a4, b4 );
   int64_t a2 = FD_KEVEN, b2 = FD_KEVEN, a6 = FD_KEVEN, b6 = FD_KEVEN;
-  c.template col2<2,6>( a2, b2, a6, b6 );
+  fd_cols_ab<CA,CB,2,6>( ca, cb, a2, b2, a6, b6 );
   int64_t a8 = FD_KEVEN, b8 = FD_KEVEN, a1 = a0 >> 26, b1 = b0 >> 26;
-  c.template col2<8,1>( a8, b8, a1, b1 );
+  fd_cols_ab<CA,CB,8,1>( ca, cb, a8, b8, a1, b1 );
   a2 += a1 >> 25; b2 += b1 >> 25;
   int64_t a5 = a4 >> 26, b5 = b4 >> 26, a3 = a2 >> 26, b3 = b2 >> 26;
-  c.template col2<5,3>( a5, b5, a3, b3 );
+  fd_cols_ab<CA,CB,5,3>( ca, cb, a5, b5, a3, b3 );
   a6 += a5 >> 25; b6 += b5 >> 25;
-  int64_t a7 = a6 >> 26, b7 = b6 >> 26;
-  c.template col<7>( a7, b7 );
+  int64_t a7 = a6 >> 26, b7 = b6 >> 26, u0 = 0, u1 = 0;
+  fd_cols_ab<CA,CB,7,-1>( ca, cb, a7, b7, u0, u1 );
   a8 += a7 >> 25; b8 += b7 >> 25;
   int64_t a9 = a8 >> 26, b9 = b8 >> 26;
-  c.template col<9>( a9, b9 );
+  fd_cols_ab<CA,CB,9,-1>( ca, cb, a9, b9, u0, u1 );
   fd_fe_limbs( oa, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
   fd_fe_limbs( ob, b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+}
+
+/* Three independent products, column by column with the three chains
+   interleaved (every MAC two instructions after its dependency). */
+template<typename C, int K, int I>
+FD_DEV void fd_cols3_step( C const & a, C const & b, C const & c, int64_t & sa, int64_t & sb, int64_t & sc ) {
+  if constexpr( I < C::template len<K>() ) {
+    sa = a.template term<K,I>( sa ); sb = b.template term<K,I>( sb ); sc = c.template term<K,I>( sc );
+  }
+}
+template<typename C, int K>
+FD_DEV void fd_cols3( C const & a, C const & b, C const & c, int64_t & sa, int64_t & sb, int64_t & sc ) {
+  fd_cols3_step<C,K,0>( a, b, c, sa, sb, sc ); fd_cols3_step<C,K,1>( a, b, c, sa, sb, sc );
+  fd_cols3_step<C,K,2>( a, b, c, sa, sb, sc ); fd_cols3_step<C,K,3>( a, b, c, sa, sb, sc );
+  fd_cols3_step<C,K,4>( a, b, c, sa, sb, sc ); fd_cols3_step<C,K,5>( a, b, c, sa, sb, sc );
+  fd_cols3_step<C,K,6>( a, b, c, sa, sb, sc ); fd_cols3_step<C,K,7>( a, b, c, sa, sb, sc );
+  fd_cols3_step<C,K,8>( a, b, c, sa, sb, sc ); fd_cols3_step<C,K,9>( a, b, c, sa, sb, sc );
+}
+template<typename C>
+FD_DEV void fd_fe_chain3( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, fd_gpu_fe_t & oc, C const & a, C const & b, C const & c ) {
+  int64_t A[10], B[10], Cc[10];
+#define FD_C3(k) fd_cols3<C,k>( a, b, c, A[k], B[k], Cc[k] )
+  A[0] = B[0] = Cc[0] = FD_KEVEN; FD_C3(0);
+  A[4] = B[4] = Cc[4] = FD_KEVEN; FD_C3(4);
+  A[2] = B[2] = Cc[2] = FD_KEVEN; FD_C3(2);
+  A[6] = B[6] = Cc[6] = FD_KEVEN; FD_C3(6);
+  A[8] = B[8] = Cc[8] = FD_KEVEN; FD_C3(8);
+  A[1] = A[0] >> 26; B[1] = B[0] >> 26; Cc[1] = Cc[0] >> 26; FD_C3(1);
+  A[5] = A[4] >> 26; B[5] = B[4] >> 26; Cc[5] = Cc[4] >> 26; FD_C3(5);
+  A[2] += A[1] >> 25; B[2] += B[1] >> 25; Cc[2] += Cc[1] >> 25;
+  A[6] += A[5] >> 25; B[6] += B[5] >> 25; Cc[6] += Cc[5] >> 25;
+  A[3] = A[2] >> 26; B[3] = B[2] >> 26; Cc[3] = Cc[2] >> 26; FD_C3(3);
+  A[7] = A[6] >> 26; B[7] = B[6] >> 26; Cc[7] = Cc[6] >> 26; FD_C3(7);
+  A[8] += A[7] >> 25; B[8] += B[7] >> 25; Cc[8] += Cc[7] >> 25;
+  A[9] = A[8] >> 26; B[9] = B[8] >> 26; Cc[9] = Cc[8] >> 26; FD_C3(9);
+#undef FD_C3
+  fd_fe_limbs( oa, A[0], A[1], A[2], A[3], A[4], A[5], A[6], A[7], A[8], A[9] );
+  fd_fe_limbs( ob, B[0], B[1], B[2], B[3], B[4], B[5], B[6], B[7], B[8], B[9] );
+  fd_fe_limbs( oc, Cc[0], Cc[1], Cc[2], Cc[3], Cc[4], Cc[5], Cc[6], Cc[7], Cc[8], Cc[9] );
 }
 
 /* Column functors for fd_fe_chain: fe_mul (AVX MUL convention, 2f_odd and
@@ -215,30 +278,6 @@ struct fd_mul_cols {
   }
 };
 
-/* Two independent products through the same chain with their column
-   multiply chains interleaved term by term.  A v_mad_i64_i32 whose 64-bit
-   accumulator was written by one of the previous two VALU instructions
-   costs hazard wait states (s_nop), so two columns of each product run
-   together where the carry order allows (col2: four chains, every MAC
-   three instructions after the one it depends on). */
-struct fd_mul_cols2 {
-  fd_mul_cols a, b;
-  template<int K, int I> FD_DEVM void t1( int64_t & sa, int64_t & sb ) const {
-    sa = a.term<K,I>( sa ); sb = b.term<K,I>( sb );
-  }
-  template<int K> FD_DEVM void col( int64_t & sa, int64_t & sb ) const {
-    t1<K,0>( sa, sb ); t1<K,1>( sa, sb ); t1<K,2>( sa, sb ); t1<K,3>( sa, sb ); t1<K,4>( sa, sb );
-    t1<K,5>( sa, sb ); t1<K,6>( sa, sb ); t1<K,7>( sa, sb ); t1<K,8>( sa, sb ); t1<K,9>( sa, sb );
-  }
-  template<int K, int L, int I> FD_DEVM void t2( int64_t & sa, int64_t & sb, int64_t & ua, int64_t & ub ) const {
-    sa = a.term<K,I>( sa ); sb = b.term<K,I>( sb ); ua = a.term<L,I>( ua ); ub = b.term<L,I>( ub );
-  }
-  template<int K, int L> FD_DEVM void col2( int64_t & sa, int64_t & sb, int64_t & ua, int64_t & ub ) const {
-    t2<K,L,0>( sa, sb, ua, ub ); t2<K,L,1>( sa, sb, ua, ub ); t2<K,L,2>( sa, sb, ua, ub ); t2<K,L,3>( sa, sb, ua, ub );
-    t2<K,L,4>( sa, sb, ua, ub ); t2<K,L,5>( sa, sb, ua, ub ); t2<K,L,6>( sa, sb, ua, ub ); t2<K,L,7>( sa, sb, ua, ub );
-    t2<K,L,8>( sa, sb, ua, ub ); t2<K,L,9>( sa, sb, ua, ub );
-  }
-};
 
 /* SQN(1) column K, term I: (operand array, limb) x (operand array, limb),
    arrays 0 = F, 1 = 2F, 2 = 19F, 3 = 38F; FD_SQ_LEN(K) terms. */
@@ -255,13 +294,19 @@ __host__ __device__ constexpr unsigned char fd_sq_tab[10][6][4] = {
   { {1,0,0,8}, {1,1,1,7}, {1,2,0,6}, {1,3,1,5}, {0,4,0,4}, {0,9,3,9} },
   { {1,0,0,9}, {1,1,0,8}, {1,2,0,7}, {1,3,0,6}, {1,4,0,5}, {0,0,0,0} } };
 
+/* A0, A1: the arrays standing for F and 2F as FIRST factors (the table
+   only has those there): F, 2F for n*f^2 with n = 1; 2F, 4F for n = 2,
+   which doubles every product, i.e. the reference's doubled column sums
+   (SQN with n = 2) carried by the same chain. */
 struct fd_sq_cols {
+  int32_t const * A0; int32_t const * A1;
   int32_t const * F; int32_t const * F2; int32_t const * F19; int32_t const * F38;
   template<int K> static constexpr int len() { return FD_SQ_LEN(K); }
   FD_DEVM int32_t const * arr( int w ) const { return w==0 ? F : w==1 ? F2 : w==2 ? F19 : F38; }
   template<int K, int I> FD_DEVM int64_t term( int64_t acc ) const {
     constexpr int wa = fd_sq_tab[K][I][0], ia = fd_sq_tab[K][I][1], wb = fd_sq_tab[K][I][2], ib = fd_sq_tab[K][I][3];
-    return fd_mad( arr( wa )[ia], arr( wb )[ib], acc );
+    static_assert( wa <= 1, "first factors are F or 2F" );
+    return fd_mad( (wa ? A1 : A0)[ia], arr( wb )[ib], acc );
   }
   template<int K> FD_DEVM int64_t col( int64_t a ) const {
     a = term<K,0>( a ); a = term<K,1>( a ); a = term<K,2>( a ); a = term<K,3>( a ); a = term<K,4>( a );
@@ -299,8 +344,8 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
 /* ha = fa*ga and hb = fb*gb, interleaved (fd_mul_cols2) */
 FD_DEV void fd_fe_mul2_pre( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int32_t const (&fa2)[10], fd_gpu_fe_t const & ga, int32_t const (&ga19)[10],
                             fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int32_t const (&fb2)[10], fd_gpu_fe_t const & gb, int32_t const (&gb19)[10] ) {
-  fd_mul_cols2 c = { { fa.v, fa2, ga.v, ga19 }, { fb.v, fb2, gb.v, gb19 } };
-  fd_fe_chain2( ha, hb, c );
+  fd_mul_cols ca = { fa.v, fa2, ga.v, ga19 }, cb = { fb.v, fb2, gb.v, gb19 };
+  fd_fe_chain2( ha, hb, ca, cb );
 }
 FD_DEV void fd_fe_mul2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, fd_gpu_fe_t const & ga,
                         fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, fd_gpu_fe_t const & gb ) {
@@ -312,42 +357,37 @@ FD_DEV void fd_fe_mul2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, fd_gpu_fe_t co
 
 /* h = n*f^2, n in {1,2}, with the AVX SQN operand convention
    (fd_ed25519_fe_avx_inl.h:592-677): 2f, 19f, 38f formed mod 2^32. */
+/* SQN operand arrays of f: F, 2F, 19F, 38F and (for n = 2) 4F, formed
+   mod 2^32 as the reference's AVX SQN (fd_ed25519_fe_avx_inl.h:592-677) */
+struct fd_sq_ops {
+  int32_t F[10], F2[10], F4[10], F19[10], F38[10];
+  FD_DEVM void set( fd_gpu_fe_t const & fe ) {
+#pragma unroll
+    for( int i=0; i<10; i++ ) {
+      F[i]   = fe.v[i];
+      F2[i]  = fd_opaque( (int32_t)(2u *(uint32_t)fe.v[i]) );
+      F4[i]  = fd_opaque( (int32_t)(4u *(uint32_t)fe.v[i]) );
+      F19[i] = fd_opaque( (int32_t)(19u*(uint32_t)fe.v[i]) );
+      F38[i] = fd_opaque( (int32_t)(38u*(uint32_t)fe.v[i]) );
+    }
+  }
+  FD_DEVM fd_sq_cols cols( int n ) const {
+    fd_sq_cols c = { n==2 ? F2 : F, n==2 ? F4 : F2, F, F2, F19, F38 };
+    return c;
+  }
+};
+
+/* h = n*f^2, n in {1,2} (SQN): the column sums (doubled for n = 2)
+   through the absorbed chain */
 FD_DEV void fd_fe_sqn( fd_gpu_fe_t & h, fd_gpu_fe_t const & fe, int n ) {
-  int32_t F[10], F2[10], F19[10], F38[10];
-#pragma unroll
-  for( int i=0; i<10; i++ ) {
-    F[i]   = fe.v[i];
-    F2[i]  = fd_opaque( (int32_t)(2u *(uint32_t)fe.v[i]) );
-    F19[i] = fd_opaque( (int32_t)(19u*(uint32_t)fe.v[i]) );
-    F38[i] = fd_opaque( (int32_t)(38u*(uint32_t)fe.v[i]) );
-  }
-  if( n==1 ) {
-    /* plain squaring: the SQN(1) column products through the absorbed chain */
-    fd_sq_cols c = { F, F2, F19, F38 };
-    fd_fe_chain( h, c );
-    return;
-  }
-  /* doubled squaring (n == 2): accumulators start at half the carry bias,
-     the sums are doubled, then the plain biased chain */
-  int64_t b[10];
-#pragma unroll
-  for( int k=0; k<10; k++ ) b[k] = n==2 ? FD_BIAS(k)/2 : FD_BIAS(k);
-  int64_t s[10];
-  s[0] = fd_opaque64( fd_mad(F[0],F[0],b[0]) );  s[0]=fd_mad(F2[1],F38[9],s[0]); s[0]=fd_mad(F2[2],F19[8],s[0]); s[0]=fd_mad(F2[3],F38[7],s[0]); s[0]=fd_mad(F2[4],F19[6],s[0]); s[0]=fd_mad(F[5],F38[5],s[0]);
-  s[1] = fd_opaque64( fd_mad(F2[0],F[1],b[1]) ); s[1]=fd_mad(F[2],F38[9],s[1]);  s[1]=fd_mad(F2[3],F19[8],s[1]); s[1]=fd_mad(F[4],F38[7],s[1]);  s[1]=fd_mad(F2[5],F19[6],s[1]);
-  s[2] = fd_opaque64( fd_mad(F2[0],F[2],b[2]) ); s[2]=fd_mad(F2[1],F[1],s[2]);   s[2]=fd_mad(F2[3],F38[9],s[2]); s[2]=fd_mad(F2[4],F19[8],s[2]); s[2]=fd_mad(F2[5],F38[7],s[2]); s[2]=fd_mad(F[6],F19[6],s[2]);
-  s[3] = fd_opaque64( fd_mad(F2[0],F[3],b[3]) ); s[3]=fd_mad(F2[1],F[2],s[3]);   s[3]=fd_mad(F[4],F38[9],s[3]);  s[3]=fd_mad(F2[5],F19[8],s[3]); s[3]=fd_mad(F[6],F38[7],s[3]);
-  s[4] = fd_opaque64( fd_mad(F2[0],F[4],b[4]) ); s[4]=fd_mad(F2[1],F2[3],s[4]);  s[4]=fd_mad(F[2],F[2],s[4]);    s[4]=fd_mad(F2[5],F38[9],s[4]); s[4]=fd_mad(F2[6],F19[8],s[4]); s[4]=fd_mad(F[7],F38[7],s[4]);
-  s[5] = fd_opaque64( fd_mad(F2[0],F[5],b[5]) ); s[5]=fd_mad(F2[1],F[4],s[5]);   s[5]=fd_mad(F2[2],F[3],s[5]);   s[5]=fd_mad(F[6],F38[9],s[5]);  s[5]=fd_mad(F2[7],F19[8],s[5]);
-  s[6] = fd_opaque64( fd_mad(F2[0],F[6],b[6]) ); s[6]=fd_mad(F2[1],F2[5],s[6]);  s[6]=fd_mad(F2[2],F[4],s[6]);   s[6]=fd_mad(F2[3],F[3],s[6]);   s[6]=fd_mad(F2[7],F38[9],s[6]); s[6]=fd_mad(F[8],F19[8],s[6]);
-  s[7] = fd_opaque64( fd_mad(F2[0],F[7],b[7]) ); s[7]=fd_mad(F2[1],F[6],s[7]);   s[7]=fd_mad(F2[2],F[5],s[7]);   s[7]=fd_mad(F2[3],F[4],s[7]);   s[7]=fd_mad(F[8],F38[9],s[7]);
-  s[8] = fd_opaque64( fd_mad(F2[0],F[8],b[8]) ); s[8]=fd_mad(F2[1],F2[7],s[8]);  s[8]=fd_mad(F2[2],F[6],s[8]);   s[8]=fd_mad(F2[3],F2[5],s[8]);  s[8]=fd_mad(F[4],F[4],s[8]);    s[8]=fd_mad(F[9],F38[9],s[8]);
-  s[9] = fd_opaque64( fd_mad(F2[0],F[9],b[9]) ); s[9]=fd_mad(F2[1],F[8],s[9]);   s[9]=fd_mad(F2[2],F[7],s[9]);   s[9]=fd_mad(F2[3],F[6],s[9]);   s[9]=fd_mad(F2[4],F[5],s[9]);
-  if( n==2 ) {
-#pragma unroll
-    for( int k=0; k<10; k++ ) s[k] += s[k];
-  }
-  fd_fe_carry( h, s );
+  fd_sq_ops o; o.set( fe );
+  fd_fe_chain( h, o.cols( n ) );
+}
+
+/* two independent squarings ha = na*fa^2, hb = nb*fb^2, interleaved */
+FD_DEV void fd_fe_sqn2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int na, fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int nb ) {
+  fd_sq_ops oa, ob; oa.set( fa ); ob.set( fb );
+  fd_fe_chain2( ha, hb, oa.cols( na ), ob.cols( nb ) );
 }
 
 FD_DEV void fd_fe_sq( fd_gpu_fe_t & h, fd_gpu_fe_t const & f ) { fd_fe_sqn( h, f, 1 ); }

@@ -518,6 +518,326 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 }
 
 /* ------------------------------------------------------------------ */
+/* Kernel 3 as a signature pool (fd_k_dsm_setup -> fd_k_dsm_pool ->
+   fd_k_dsm_final).  The uniform step above pays for both op kinds on
+   every lane.  Here each wave owns a pool of FD_POOL signatures whose p1p1
+   states live in LDS; every iteration it picks ONE op kind and steps up to
+   64 signatures whose next op is of that kind, so a doubling costs its own
+   3 multiplies + 4 squarings (no T product, no selects) and only additions
+   pay 8 multiplies.  Additions wait in the pool until 64 of them are
+   pending (or nothing else is); among more than 64 candidates the ones
+   furthest from the end of their stream go first, which keeps the pool
+   draining evenly (99% lane occupancy in simulation with 128 slots; a
+   pool that is refilled while it drains, or one much smaller than 2 x 64,
+   loses most of the gain to partly filled steps).  Op sequence, operands
+   and operand order of every product are those of the uniform kernel, so
+   results are limb-identical. */
+
+
+/* Ai table for one signature: the uniform kernel's precompute
+   (avx/fd_ed25519_ge.c:423-481), one lane per signature */
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_dsm_setup( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+                int32_t const * __restrict__ pts, int32_t * __restrict__ tab, int portable ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  if( status[i] != FD_ST_PENDING || pstat[i] != FD_PT_OK || (!portable && pstat[n+i] != FD_PT_OK) ) return;
+  uint64_t m = 2*n;
+  fe4 vr, vt, vu;
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + i]);
+    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + i];
+    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + i];
+    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + i]);
+  }
+  fe4 d111;
+#pragma unroll
+  for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
+  d111.l[3] = FD_GPU_D2;
+  v_mul( vu, vr, d111 ); v_subadd_12( vu );
+  fd_tab_store( tab, i, 0, vu );
+  v_p2_dbl( vt, vr.l[2], vr.l[1], vr.l[0] );
+  {
+    fe4 a, b;
+    a.l[0]=vt.l[3]; a.l[1]=vt.l[2]; a.l[2]=vt.l[3]; a.l[3]=vt.l[1];
+    b.l[0]=vt.l[2]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
+    v_mul( vr, a, b );
+  }
+  v_subadd_12( vr );
+  for( int e=0; e<7; e++ ) {
+    v_mul( vt, vr, vu );
+    v_sub_mix( vt );
+    fe4 a, b;
+    a.l[0]=vt.l[2]; a.l[1]=vt.l[3]; a.l[2]=vt.l[2]; a.l[3]=vt.l[1];
+    b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
+    v_mul( vt, a, b );
+    v_mul( vu, vt, d111 ); v_subadd_12( vu );
+    fd_tab_store( tab, i, e+1, vu );
+  }
+}
+
+/* D step: p1p1 -> p2 ([X,Y,Z] = [t0 t3, t1 t2, t2 t3], avx/fd_ed25519_ge.c:
+   521-522), then DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)) (:493-498) */
+FD_DEV void fd_pool_dbl( fe4 & vt ) {
+  fe Z, Y, X;
+  {
+    int32_t g3[10], f2[10], f0[10], f1[10], g2[10];
+    fd_fe_pre_g( g3, vt.l[3] ); fd_fe_pre_f( f2, vt.l[2] ); fd_fe_pre_f( f0, vt.l[0] );
+    fd_fe_pre_f( f1, vt.l[1] ); fd_fe_pre_g( g2, vt.l[2] );
+    fd_mul_cols cz = { vt.l[2].v, f2, vt.l[3].v, g3 }, cx = { vt.l[0].v, f0, vt.l[3].v, g3 }, cy = { vt.l[1].v, f1, vt.l[2].v, g2 };
+    fd_fe_chain3( Z, X, Y, cz, cx, cy );
+  }
+  fe xy; fd_fe_add( xy, X, Y );
+  fd_fe_sqn2( vt.l[0], xy, 1, vt.l[1], Y, 1 );
+  fd_fe_sqn2( vt.l[2], X, 1, vt.l[3], Z, 2 );
+  v_dbl_mix( vt );
+}
+
+/* A step: p1p1 -> p3 ([Z,Y,X,T], :506-508) then
+   SUB_MIX(MUL(SUBADD_12(p3), E)) with the signed digit's entry E */
+FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, int32_t const * bi ) {
+  /* the entry loads go out first: the conversion products hide their latency */
+  fe E0, E1, E2, E3;
+  fd_entry( E0, E1, E2, E3, op, tab_i, bi );
+  fe Z, Y, X, T;
+  {
+    int32_t g3[10], f0[10];
+    fd_fe_pre_g( g3, vt.l[3] );
+    fd_fe_pre_f( f0, vt.l[0] );
+    { int32_t f2[10]; fd_fe_pre_f( f2, vt.l[2] );
+      fd_fe_mul2_pre( Z, vt.l[2], f2, vt.l[3], g3, X, vt.l[0], f0, vt.l[3], g3 ); }
+    { int32_t f1[10], g2[10], g1[10]; fd_fe_pre_f( f1, vt.l[1] ); fd_fe_pre_g( g2, vt.l[2] ); fd_fe_pre_g( g1, vt.l[1] );
+      fd_fe_mul2_pre( Y, vt.l[1], f1, vt.l[2], g2, T, vt.l[0], f0, vt.l[1], g1 ); }
+  }
+  fe h0, h1, h2, h3;   /* P, Q, R, S */
+  {
+    fe xy, ymx;
+    fd_fe_add( xy, X, Y );
+    fd_fe_sub( ymx, Y, X );
+    fd_fe_mul2( h0, xy, E2, h1, Z, E0 );
+    fd_fe_mul2( h2, ymx, E1, h3, T, E3 );
+  }
+  uint32_t mp = (uint32_t)fd_opaque( -(int32_t)!((op >> 5) & 1) );   /* positive digit: swap out lanes 2,3 */
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    uint32_t P = h0.v[k], Q = h1.v[k], R = h2.v[k], S = h3.v[k];
+    uint32_t Q2 = 2u*Q, o2 = Q2 - S, o3 = Q2 + S;
+    vt.l[0].v[k] = (int32_t)(P - R);
+    vt.l[1].v[k] = (int32_t)(P + R);
+    vt.l[2].v[k] = (int32_t)fd_sel( mp, o3, o2 );
+    vt.l[3].v[k] = (int32_t)fd_sel( mp, o2, o3 );
+  }
+}
+
+/* index of the r-th (0-based) set bit of x, r < popcount(x): the wave
+   shares x (scalar), lanes ask for different r */
+FD_DEV uint32_t fd_nth_bit( uint64_t x, uint32_t r ) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t nlo = (uint32_t)__builtin_popcount( lo );
+  uint32_t w = r < nlo ? lo : hi, base = r < nlo ? 0u : 32u;
+  r = r < nlo ? r : r - nlo;
+  uint32_t pos = 0;
+#pragma unroll
+  for( uint32_t step=16; step; step>>=1 ) {
+    uint32_t below = w & ((1u << (pos + step)) - 1u);   /* pos + step <= 31 */
+    pos += (uint32_t)__builtin_popcount( below ) <= r ? step : 0u;
+  }
+  return base + pos;
+}
+
+FD_DEV uint32_t fd_lanes_below( uint64_t m ) {
+  return __builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
+}
+FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
+
+/* 128 slots per wave: lane l owns slots l and l+64 and keeps their
+   (t << 8 | op) in registers; the p1p1 states are in LDS (20 limb pairs x
+   128 slots x 8 B = 20 KiB per wave, 8 waves = the CU's 160 KiB).  Slot s holds signature
+   gw + s*nwaves. */
+#define FD_POOL 128
+struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS accesses (64 banks) */
+
+FD_DEV void fd_pool_ld( fe4 & vt, fd_pool_lds const & L, uint32_t s ) {
+#pragma unroll
+  for( int k=0; k<20; k++ ) {
+    uint64_t x = L.st[k][s];
+    vt.l[(2*k)/10].v[(2*k)%10]     = (int32_t)(uint32_t)x;
+    vt.l[(2*k+1)/10].v[(2*k+1)%10] = (int32_t)(uint32_t)(x >> 32);
+  }
+}
+FD_DEV void fd_pool_st( fd_pool_lds & L, uint32_t s, fe4 const & vt ) {
+#pragma unroll
+  for( int k=0; k<20; k++ )
+    L.st[k][s] = (uint64_t)(uint32_t)vt.l[(2*k)/10].v[(2*k)%10] | ((uint64_t)(uint32_t)vt.l[(2*k+1)/10].v[(2*k+1)%10] << 32);
+}
+
+extern "C" __global__ void __launch_bounds__(256, 2)
+fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+               uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+               int32_t const * __restrict__ tab, int32_t * __restrict__ fin, int portable, uint32_t nwaves ) {
+  __shared__ fd_pool_lds pool[4];
+  uint32_t gw   = blockIdx.x*4u + (threadIdx.x >> 6);
+  uint32_t lane = threadIdx.x & 63u;
+  if( gw >= nwaves ) return;
+  fd_pool_lds & L = pool[threadIdx.x >> 6];
+  uint64_t m = 2*n;
+  int const EMPTY = FD_OPS_MAX << 8;
+
+  /* slot init: pending signatures start at their op stream, state p1p1
+     [0,1,1,1] */
+  int mt[2];
+#pragma unroll
+  for( int j=0; j<2; j++ ) {
+    uint32_t s = lane + 64u*(uint32_t)j;
+    uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
+    int mm = EMPTY;
+    if( sg < n ) {
+      int st = status[sg], pa = pstat[sg], pr = portable ? FD_PT_OK : pstat[n+sg];
+      if( st == FD_ST_PENDING && pa == FD_PT_OK && pr == FD_PT_OK ) {
+        int t = op_start[sg];
+        mm = (t << 8) | (int)ops[(uint64_t)t*n + sg];
+      }
+    }
+    mt[j] = mm;
+    fe4 id;
+#pragma unroll
+    for( int l=0; l<4; l++ ) fd_fe_set( id.l[l], l ? 1 : 0 );
+    fd_pool_st( L, s, id );
+  }
+  fd_mem_fence();
+
+  for(;;) {
+    int m0 = mt[0], m1 = mt[1];
+    int t0 = m0 >> 8, t1 = m1 >> 8;
+    int l0 = t0 < FD_OPS_MAX, l1 = t1 < FD_OPS_MAX;
+    int a0 = l0 && (m0 & FD_OP_ADD), a1 = l1 && (m1 & FD_OP_ADD);
+    uint32_t nA = (uint32_t)(__popcll( __ballot( a0 ) ) + __popcll( __ballot( a1 ) ));
+    uint32_t nL = (uint32_t)(__popcll( __ballot( l0 ) ) + __popcll( __ballot( l1 ) ));
+    if( !nL ) break;
+    int kind = nA >= 64u || nA == nL;          /* 1: additions, 0: doublings */
+    int c0 = kind ? a0 : (l0 && !a0), c1 = kind ? a1 : (l1 && !a1);
+    uint64_t x0 = __ballot( c0 ), x1 = __ballot( c1 );
+    uint32_t nc = (uint32_t)(__popcll( x0 ) + __popcll( x1 ));
+    if( nc > 64u ) {
+      /* the 64 candidates with the smallest t (furthest from the end of
+         their streams): lo = largest bound with at most 64 candidates
+         below it, ties at lo taken in slot order */
+      int lo = 0, hi = FD_OPS_MAX + 1;         /* 10 halvings close 769 (unrolled, branch-free) */
+#pragma unroll
+      for( int it=0; it<10; it++ ) {
+        int mid = (lo + hi) >> 1;
+        uint32_t c = (uint32_t)(__popcll( __ballot( c0 && t0 < mid ) ) + __popcll( __ballot( c1 && t1 < mid ) ));
+        int ok = c <= 64u;
+        lo = ok ? mid : lo;
+        hi = ok ? hi : mid;
+      }
+      uint64_t y0 = __ballot( c0 && t0 < lo ), y1 = __ballot( c1 && t1 < lo );
+      uint64_t z0 = __ballot( c0 && t0 == lo ), z1 = __ballot( c1 && t1 == lo );
+      uint32_t need = 64u - (uint32_t)(__popcll( y0 ) + __popcll( y1 ));
+      uint32_t nz0 = (uint32_t)__popcll( z0 );
+      int k0 = ((z0 >> lane) & 1ULL) && fd_lanes_below( z0 ) < need;
+      int k1 = ((z1 >> lane) & 1ULL) && nz0 + fd_lanes_below( z1 ) < need;
+      x0 = y0 | __ballot( k0 );
+      x1 = y1 | __ballot( k1 );
+      nc = 64u;
+    }
+    uint32_t n0 = (uint32_t)__popcll( x0 );
+
+    /* lane l steps the l-th selected slot (bank-0 slots first) */
+    uint32_t bank = lane >= n0;
+    uint32_t j    = fd_nth_bit( bank ? x1 : x0, bank ? lane - n0 : lane );
+    int act = lane < nc;
+    j = act ? j : lane;
+    uint32_t s = j + 64u*bank;
+    int ma = __shfl( m0, (int)j, 64 ), mb = __shfl( m1, (int)j, 64 );
+    int mm = bank ? mb : ma;
+    int nm = mm;
+    if( act ) {
+      int t = mm >> 8, op = mm & 255;
+      uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
+      int tn = t + 1;
+      int opn = tn < FD_OPS_MAX ? (int)ops[(uint64_t)tn*n + sg] : 0;   /* prefetch */
+      fe4 vt;
+      fd_pool_ld( vt, L, s );
+      if( kind ) fd_pool_add( vt, op, tab + sg*FD_TAB_SIG, fd_gpu_bi_tab );
+      else       fd_pool_dbl( vt );
+      if( tn < FD_OPS_MAX ) {
+        fd_pool_st( L, s, vt );
+        nm = (tn << 8) | opn;
+      } else {
+#pragma unroll
+        for( int k=0; k<40; k++ ) fin[(uint64_t)k*m + sg] = vt.l[k/10].v[k%10];
+        nm = EMPTY;
+      }
+    }
+    fd_mem_fence();
+    /* owners take their stepped slots' new (t, op) from the stepping lanes */
+    int r0 = (int)fd_lanes_below( x0 ), r1 = (int)(n0 + fd_lanes_below( x1 ));
+    int v0 = __shfl( nm, r0 & 63, 64 ), v1 = __shfl( nm, r1 & 63, 64 );
+    if( (x0 >> lane) & 1ULL ) mt[0] = v0;
+    if( (x1 >> lane) & 1ULL ) mt[1] = v1;
+    fd_mem_fence();
+  }
+}
+
+/* final p1p1 -> p2 and the compare (uniform kernel's tail), one lane per
+   signature; fin holds the pool's final p1p1 states */
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_dsm_final( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+                int32_t const * __restrict__ pts, int32_t * __restrict__ out,
+                uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  uint64_t m = 2*n;
+  int st = status[i];
+  int pa = pstat[i], pr = portable ? FD_PT_OK : pstat[n+i];
+  int code;
+  if( st != FD_ST_PENDING )                        code = st;
+  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
+  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
+  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
+  else                                             code = FD_ST_PENDING;
+  if( code != FD_ST_PENDING ) { out[i] = code; return; }
+  fe4 vt;
+#pragma unroll
+  for( int k=0; k<40; k++ ) vt.l[k/10].v[k%10] = pts[(uint64_t)k*m + i];
+  fe X, Y, Z;
+  fd_fe_mul( X, vt.l[0], vt.l[3] );
+  fd_fe_mul( Y, vt.l[1], vt.l[2] );
+  fd_fe_mul( Z, vt.l[2], vt.l[3] );
+  if( portable ) {
+    fe zi, x, y;
+    fd_fe_invert( zi, Z );
+    fd_fe_mul( x, X, zi );
+    fd_fe_mul( y, Y, zi );
+    uint32_t enc[8];
+    fd_fe_tobytes32( enc, y );
+    enc[7] ^= (uint32_t)fd_fe_isnegative( x ) << 31;
+    uint32_t rw[8];
+    fd_ld32( rw, blob + desc[i].sig_off );
+    uint32_t diff = 0;
+#pragma unroll
+    for( int k=0; k<8; k++ ) diff |= enc[k] ^ rw[k];
+    out[i] = diff ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS;
+    return;
+  }
+  fe rx, ry;
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    rx.v[k] = pts[(uint64_t)( 0+k)*m + n + i];
+    ry.v[k] = pts[(uint64_t)(10+k)*m + n + i];
+  }
+  fe xz, yz;
+  fd_fe_mul( xz, Z, rx );
+  fd_fe_mul( yz, Z, ry );
+  int eq = 1;
+#pragma unroll
+  for( int k=0; k<8; k++ ) eq &= (xz.v[k] == X.v[k]) & (yz.v[k] == Y.v[k]);
+  out[i] = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+/* ------------------------------------------------------------------ */
 /* SHA-512 / SHA-384 batch (the ballet batch API's GPU backend,
    src/ballet/sha512/fd_sha512.h:223-294): one lane per message
    blob[msg_off..+msg_sz), digest to out[64 i..] (48 bytes for SHA-384). */
@@ -560,7 +880,7 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
 
 extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                    hipEvent_t const * ev, int mode ) {
+                                                    hipEvent_t const * ev, int mode, uint64_t pool_min ) {
   if( !n ) return hipSuccess;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   unsigned nb  = (unsigned)((n + 255) / 256);
@@ -571,13 +891,22 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   if( ev ) hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable );
   if( ev ) hipEventRecord( ev[2], stream );
-  hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
-                      blob, desc, portable );
+  if( n >= pool_min ) {
+    uint32_t nw = (uint32_t)((n + FD_POOL - 1) / FD_POOL);  /* one full pool per wave */
+    hipLaunchKernelGGL( fd_k_dsm_setup, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->tab, portable );
+    hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
+                        w->tab, w->pts, portable, nw );
+    hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable );
+  } else {
+    hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
+                        blob, desc, portable );
+  }
   if( ev ) hipEventRecord( ev[3], stream );
   return hipGetLastError();
 }
 
 extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
-                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode ) {
-  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode );
+                                              fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
+                                              uint64_t pool_min ) {
+  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode, pool_min );
 }

@@ -174,6 +174,15 @@ fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * gpu, int mode );
 int fd_ed25519_gpu_mode    ( fd_ed25519_gpu_t const * gpu );
 
+/* DSM schedule (results are identical either way): batches of at least
+   pool_min signatures (default 262144) run the double-scalar
+   multiplication as per-wave signature pools that step 64 signatures of
+   one op kind at a time; smaller batches step every lane every
+   iteration (more waves in flight, lower latency).  0 = always pooled,
+   ULONG_MAX = never. */
+int           fd_ed25519_gpu_set_dsm_pool_min( fd_ed25519_gpu_t * gpu, unsigned long pool_min );
+unsigned long fd_ed25519_gpu_dsm_pool_min    ( fd_ed25519_gpu_t const * gpu );
+
 /* Zero-copy staging: lend the pinned blob (max_blob + 64 bytes) and
    descriptor (max_sigs) buffers of a free ring slot.  The caller builds
    the batch in place and passes the same pointers to

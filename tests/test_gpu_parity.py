@@ -175,3 +175,38 @@ def test_device_resident(engine):
     engine.verify_dev(len(b), blob.data_ptr(), desc.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert (out.cpu().numpy() == exp).all()
+
+
+@pytest.fixture(scope="module")
+def pooled():
+    """an engine that runs the pooled DSM (fd_k_dsm_pool) for every batch"""
+    e = fa.Engine(0, 1 << 18, 1 << 28)
+    e.dsm_pool_min = 0
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
+def test_pooled_dsm_golden_corpora(pooled, name):
+    """the pooled schedule steps signatures in a data-dependent order; the
+    codes must still be the reference's"""
+    b, exp = load_corpus(name)
+    got = pooled.verify_packed(b.blob, b.desc)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("n", [1, 63, 129, 4096 + 77, 40000])
+def test_pooled_equals_uniform(engine, pooled, n):
+    """ragged pools (n not a multiple of 128, fewer slots than lanes) and
+    several waves: pooled and uniform schedules give identical codes on a
+    mixed valid / invalid batch"""
+    base, _ = load_corpus("adversarial")
+    b = base.tile(int(np.ceil(n / len(base))))
+    b.desc = b.desc[:n]
+    engine.dsm_pool_min = 1 << 62
+    a = engine.verify_packed(b.blob, b.desc)
+    p = pooled.verify_packed(b.blob, b.desc)
+    assert (a == p).all(), np.nonzero(a != p)[0][:10]
+    assert engine.dsm_pool_min == 1 << 62
+    engine.dsm_pool_min = 262144
