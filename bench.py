@@ -36,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BATCH_SIGS = 4096
-STEP_BATCHES = 64
+STEP_BATCHES = 256
 UNIQUE_SIGS = 65536
 
 # ---- algorithmic work model --------------------------
@@ -57,12 +57,18 @@ SLOT_SHA_BLOCK = 4900
 # per-verify reference op counts (251.5 doublings and
 # 84.9 additions per verify, measured on the reference's slide statistics)
 N_DBL, N_ADD = 251.5, 84.9
-# fd_k_dsm: Ai table (avx/fd_ed25519_ge.c:423-481: 92 mul, 3 sq, 1 sq2);
-#   each doubling SQN(1,1,1,2) + one 4-lane conversion MUL; each addition
-#   one 4-lane MUL + conversion MUL; compare 2 mul (fd_ed25519_user.c:419-427);
-#   lane mixes DBL_MIX+X+Y 50, SUBADD_12+SUB_MIX 70 int32 ops.
-SLOTS_DSM = ((92 + 4 * N_DBL + 8 * N_ADD + 2) * SLOT_MUL + (3 + 3 * N_DBL) * SLOT_SQ
-             + (1 + N_DBL) * SLOT_SQ2 + 50 * N_DBL + 70 * N_ADD)
+# DSM, split as the engine runs it (avx/fd_ed25519_ge.c:423-523,
+#   fd_ed25519_user.c:419-427):
+#   fd_k_dsm_setup: Ai table, 92 mul + 3 sq + 1 sq2 + 8 x 30 mix ops;
+#   fd_k_dsm_pool:  each doubling SQN(1,1,1,2) + one 4-lane conversion MUL,
+#                   each addition one 4-lane MUL + conversion MUL, lane mixes
+#                   DBL_MIX+X+Y 50, SUBADD_12+SUB_MIX 70 int32 ops;
+#   fd_k_dsm_final: p2 conversion 3 mul + compare 2 mul.
+SLOTS_DSM_SETUP = 92 * SLOT_MUL + 3 * SLOT_SQ + SLOT_SQ2 + 240
+SLOTS_DSM_LOOP = ((4 * N_DBL + 8 * N_ADD) * SLOT_MUL + 3 * N_DBL * SLOT_SQ + N_DBL * SLOT_SQ2
+                  + 50 * N_DBL + 70 * N_ADD)
+SLOTS_DSM_FINAL = 5 * SLOT_MUL
+SLOTS_DSM = SLOTS_DSM_SETUP + SLOTS_DSM_LOOP + SLOTS_DSM_FINAL
 # fd_k_decomp, per point (avx/fd_ed25519_ge.c:222-299 + fd_ed25519_ge.c:11-66):
 #   264 sq + 3 sq2 (pow22523 251, 4 around it, small-order 3 x 4) and 32 mul,
 #   + frombytes 60 + 3 canonical reductions x 40; two points per verify.
@@ -216,7 +222,7 @@ def main():
     if rank == 0 and world == 1:
         # per-kernel durations over the same launches, on the launch stream
         reps = max(3, min(a.steps, 10))
-        ks = np.zeros(3)
+        ks = np.zeros(len(fa.Engine.KERNELS))
         for _ in range(reps):
             ks += eng.verify_dev_timed(n_step, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), stream)
         ks /= reps
@@ -224,10 +230,12 @@ def main():
         blocks = float(np.mean([sha_blocks(int(m)) for m in msz]))
         ops = {"fd_k_prep": (SLOT_SHA_BLOCK * blocks + SLOTS_PREP_FIXED) * n_step,
                "fd_k_decomp": SLOTS_DECOMP * n_step,
-               "fd_k_dsm": SLOTS_DSM * n_step}
+               "fd_k_dsm_setup": SLOTS_DSM_SETUP * n_step,
+               "fd_k_dsm_pool": SLOTS_DSM_LOOP * n_step,
+               "fd_k_dsm_final": SLOTS_DSM_FINAL * n_step}
         kern = {}
         for name, ms in zip(fa.Engine.KERNELS, ks):
-            ach = ops[name] / (ms * 1e-3) / 1e12
+            ach = ops[name] / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
             kern[name] = {"ms": float(ms), "achieved_Tops": ach, "frac": ach * 1e12 / PEAK_INT32_OPS}
         dom = max(kern, key=lambda k: kern[k]["ms"])
         traffic = None

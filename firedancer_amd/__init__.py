@@ -223,7 +223,7 @@ class Engine:
         if err:
             raise EngineError(f"verify_dev: {strerror(err)}: {last_error()}")
 
-    KERNELS = ("fd_k_prep", "fd_k_decomp", "fd_k_dsm")
+    KERNELS = ("fd_k_prep", "fd_k_decomp", "fd_k_dsm_setup", "fd_k_dsm_pool", "fd_k_dsm_final")
 
     def verify_dev_timed(self, n: int, d_blob: int, d_desc: int, d_out: int, stream: int = 0) -> np.ndarray:
         """verify_dev with per-kernel HIP-event durations (ms), in KERNELS order."""

@@ -891,17 +891,23 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   if( ev ) hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable );
   if( ev ) hipEventRecord( ev[2], stream );
+  /* phases 3-5: DSM setup (Ai tables), DSM main loop, final compare; the
+     uniform schedule is one kernel (its time lands in phase 4) */
   if( n >= pool_min ) {
     uint32_t nw = (uint32_t)((n + FD_POOL - 1) / FD_POOL);  /* one full pool per wave */
     hipLaunchKernelGGL( fd_k_dsm_setup, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->tab, portable );
+    if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
                         w->tab, w->pts, portable, nw );
+    if( ev ) hipEventRecord( ev[4], stream );
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable );
   } else {
+    if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
                         blob, desc, portable );
+    if( ev ) hipEventRecord( ev[4], stream );
   }
-  if( ev ) hipEventRecord( ev[3], stream );
+  if( ev ) hipEventRecord( ev[5], stream );
   return hipGetLastError();
 }
 

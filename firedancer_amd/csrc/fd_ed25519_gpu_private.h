@@ -7,7 +7,7 @@
 
 /* Per-batch HBM working set, SoA [field][item] (sizes for capacity N):
      status   int32 [N]          prep result (S check) or pending
-     ops      uint8 [768][N]     per-signature DSM op stream, right aligned
+     ops      uint8 [512][N]     per-signature DSM op stream, right aligned
      op_start int32 [N]          first op index (FD_OPS_MAX if none)
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
@@ -24,10 +24,10 @@ typedef struct fd_ed25519_gpu_work {
 
 /* bytes of HBM working set per signature of capacity */
 /* number of kernels in one launch (timed API) */
-#define FD_ED25519_GPU_KERNEL_CNT 3
+#define FD_ED25519_GPU_KERNEL_CNT 5
 
 /* op stream capacity: 256 doublings + at most 256 adds per scalar */
-#define FD_OPS_MAX 768
+#define FD_OPS_MAX 512
 
 /* Ai / Bi table entry geometry (dwords) */
 #define FD_TAB_LANE  12

@@ -200,9 +200,12 @@ fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * gpu, void const * blob );
 /* Diagnostics: fd_ed25519_gpu_verify_dev with HIP events around each of
    the engine's fd_ed25519_gpu_kernel_cnt() kernels on `stream`; blocks
    until done and writes each kernel's duration (ms) to kernel_ms[].
-   Kernel order: prep (SHA-512, mod L, recoding), decomp (point
-   decompression + small-order test), dsm (double-scalar multiplication
-   + compare). */
+   Phase order: prep (SHA-512, mod L, recoding), decomp (point
+   decompression + small-order test), dsm_setup (per-signature Ai
+   tables), dsm (double-scalar multiplication main loop), dsm_final
+   (p2 conversion + compare).  With the uniform DSM schedule (batches
+   below the pool threshold) the DSM is one kernel, timed as phase dsm,
+   and the setup / final phases read 0. */
 int
 fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t *            gpu,
                                  unsigned long                 n,

@@ -13,7 +13,7 @@ import pytest
 from conftest import P
 from test_fe_host import harness  # noqa: F401  (module fixture)
 
-FD_OPS_MAX = 768
+FD_OPS_MAX = 512
 L = 2**252 + 27742317777372353535851937790883648493
 
 

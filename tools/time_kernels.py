@@ -26,7 +26,7 @@ def main():
     s = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(3):
         eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
-    ks = np.zeros(3)
+    ks = np.zeros(len(fa.Engine.KERNELS))
     reps = 10
     for _ in range(reps):
         ks += eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
