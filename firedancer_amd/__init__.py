@@ -144,6 +144,10 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_set_dsm_pool_min.restype = ip
         L.fd_ed25519_gpu_dsm_pool_min.argtypes = [vp]
         L.fd_ed25519_gpu_dsm_pool_min.restype = ul
+        L.fd_ed25519_gpu_set_dsm_quad_max.argtypes = [vp, ul]
+        L.fd_ed25519_gpu_set_dsm_quad_max.restype = ip
+        L.fd_ed25519_gpu_dsm_quad_max.argtypes = [vp]
+        L.fd_ed25519_gpu_dsm_quad_max.restype = ul
         L.fd_ed25519_gpu_multi_new.argtypes = [vp, ip, ul, ul]
         L.fd_ed25519_gpu_multi_new.restype = vp
         L.fd_ed25519_gpu_multi_delete.argtypes = [vp]
@@ -285,6 +289,16 @@ class Engine:
     def dsm_pool_min(self, n: int) -> None:
         if lib().fd_ed25519_gpu_set_dsm_pool_min(self._h, n):
             raise EngineError("set_dsm_pool_min")
+
+    @property
+    def dsm_quad_max(self) -> int:
+        """smaller batches of at most this many signatures take the quad-lane DSM"""
+        return lib().fd_ed25519_gpu_dsm_quad_max(self._h)
+
+    @dsm_quad_max.setter
+    def dsm_quad_max(self, n: int) -> None:
+        if lib().fd_ed25519_gpu_set_dsm_quad_max(self._h, n):
+            raise EngineError("set_dsm_quad_max")
 
     @property
     def depth(self) -> int:

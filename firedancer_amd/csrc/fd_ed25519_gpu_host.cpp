@@ -52,6 +52,7 @@ struct fd_ed25519_gpu {
   int           depth;
   int           mode;     /* FD_ED25519_GPU_MODE_* */
   unsigned long pool_min; /* batches >= this take the pooled DSM */
+  unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
@@ -111,6 +112,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   }
   fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
+  g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   unsigned long blob_cap = max_blob + FD_BLOB_PAD;
   HIPCHK( hipSetDevice( device ) );
@@ -174,6 +176,13 @@ extern "C" int fd_ed25519_gpu_set_dsm_pool_min( fd_ed25519_gpu_t * g, unsigned l
   return 0;
 }
 extern "C" unsigned long fd_ed25519_gpu_dsm_pool_min( fd_ed25519_gpu_t const * g ) { return g ? g->pool_min : 0UL; }
+extern "C" int fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * g, unsigned long n ) {
+  if( !g ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  g->quad_max = n;
+  return 0;
+}
+extern "C" unsigned long fd_ed25519_gpu_dsm_quad_max( fd_ed25519_gpu_t const * g ) { return g ? g->quad_max : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
 
@@ -218,7 +227,7 @@ extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n,
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->mode, g->pool_min );
+  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->mode, g->pool_min, g->quad_max );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   return 0;
 }
@@ -230,7 +239,7 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev, g->mode, g->pool_min );
+  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev, g->mode, g->pool_min, g->quad_max );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   if( (e = hipEventSynchronize( g->kev[FD_ED25519_GPU_KERNEL_CNT] )) != hipSuccess ) return fd_gpu_fail( "sync", e );
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
@@ -262,7 +271,7 @@ static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsi
     return fd_gpu_fail( "H2D blob", e );
   if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "H2D desc", e );
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream, g->mode, g->pool_min )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );

@@ -518,6 +518,207 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 }
 
 /* ------------------------------------------------------------------ */
+/* Kernel 3 for latency (small batches): one QUAD of lanes per signature,
+   lane q of the quad carrying the AVX path's lane q (one wl_t x 10 field
+   element of the reference's 4-lane vectors, fd_ed25519_fe_avx.h:32-69).
+   A 4-lane MUL is then one product per lane, the lane permutations of
+   the reference (perm / DBL_MIX / SUB_MIX / SUBADD_12) are DPP quad_perm
+   moves, and a signature's serial chain per step is two products instead
+   of eight: a 4,096-signature batch runs as 256 waves instead of 64.
+   Per signature the Ai table and the op stream live in LDS.  Same
+   products, same operands and operand order as fd_k_dsm (limb-identical
+   codes, tests/test_gpu_parity.py::test_quad_*). */
+
+#define FD_QP(a,b,c,d) ((a)|((b)<<2)|((c)<<4)|((d)<<6))
+#define FD_QDEV static __device__ __forceinline__
+
+template<int CTRL> FD_QDEV int32_t fd_qperm( int32_t x ) {
+  return __builtin_amdgcn_mov_dpp( x, CTRL, 0xF, 0xF, true );
+}
+template<int CTRL> FD_QDEV void fd_fe_qperm( fe & o, fe const & x ) {
+#pragma unroll
+  for( int k=0; k<10; k++ ) o.v[k] = fd_qperm<CTRL>( x.v[k] );
+}
+/* ((x & m) ^ s) - s: x, 0, -x or (m = 0, s = ~0) 0, for masks in {0, ~0} */
+FD_QDEV uint32_t fd_qterm( uint32_t x, uint32_t m, uint32_t s ) { return ((x & m) ^ s) - s; }
+
+/* SUBADD_12 across the quad: [a, b-c, b+c, d] */
+FD_QDEV void fd_q_subadd12( fe & x, uint32_t m12, uint32_t s1 ) {
+  fe p; fd_fe_qperm<FD_QP(0,2,1,3)>( p, x );
+#pragma unroll
+  for( int k=0; k<10; k++ ) x.v[k] = (int32_t)((uint32_t)x.v[k] + fd_qterm( (uint32_t)p.v[k], m12, s1 ));
+}
+/* SUB_MIX: [c-b, c+b, 2a-d, 2a+d] */
+FD_QDEV void fd_q_submix( fe & x, uint32_t sh, uint32_t se ) {
+  fe u, w; fd_fe_qperm<FD_QP(2,2,0,0)>( u, x ); fd_fe_qperm<FD_QP(1,1,3,3)>( w, x );
+#pragma unroll
+  for( int k=0; k<10; k++ ) x.v[k] = (int32_t)(((uint32_t)u.v[k] << sh) + fd_qterm( (uint32_t)w.v[k], ~0u, se ));
+}
+/* DBL_MIX: [a-b-c, b+c, b-c, d-b+c] */
+FD_QDEV void fd_q_dblmix( fe & x, uint32_t m03, uint32_t s02 ) {
+  fe b, c; fd_fe_qperm<FD_QP(1,1,1,1)>( b, x ); fd_fe_qperm<FD_QP(2,2,2,2)>( c, x );
+#pragma unroll
+  for( int k=0; k<10; k++ )
+    x.v[k] = (int32_t)(((uint32_t)x.v[k] & m03) + fd_qterm( (uint32_t)b.v[k], ~0u, m03 ) + fd_qterm( (uint32_t)c.v[k], ~0u, s02 ));
+}
+
+#define FD_QSIGS 16   /* signatures per 64-lane wave */
+struct fd_quad_lds {
+  int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
+  uint8_t ops[FD_OPS_MAX][FD_QSIGS];
+};
+
+FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
+  int4 * q = (int4 *)p;
+  q[0] = make_int4( v.v[0], v.v[1], v.v[2], v.v[3] );
+  q[1] = make_int4( v.v[4], v.v[5], v.v[6], v.v[7] );
+  q[2] = make_int4( v.v[8], v.v[9], 0, 0 );
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+               int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+               int32_t * __restrict__ out ) {
+  __shared__ __attribute__((aligned(16))) fd_quad_lds L;
+  uint32_t lane = threadIdx.x;
+  uint32_t q    = lane & 3u, ls = lane >> 2;
+  uint64_t sig0 = (uint64_t)blockIdx.x * FD_QSIGS;
+  uint64_t i    = sig0 + ls;
+  int live = i < n;
+  uint64_t ii = live ? i : 0;
+  uint64_t m = 2*n;
+  int st = status[ii];
+  int pa = pstat[ii], pr = pstat[n+ii];
+  int code;
+  /* error precedence (fd_ed25519_user.c:372-403) */
+  if( st != FD_ST_PENDING )                        code = st;
+  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
+  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
+  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
+  else                                             code = FD_ST_PENDING;
+  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
+
+  /* lane q of vr = [Z, Y, -X, -T] of A (fd_ed25519_user.c:408-409), and
+     this lane's half of the final compare's (r.x, r.y) */
+  uint32_t const comp = q==0u ? 20u : q==1u ? 10u : q==2u ? 0u : 30u;
+  fe r, rr;
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    int32_t x = pts[(uint64_t)(comp+k)*m + ii];
+    r.v[k]  = q >= 2u ? (int32_t)(0u - (uint32_t)x) : x;
+    rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
+  }
+
+  /* op streams of the wave's 16 signatures -> LDS (rows from the wave's
+     first op on) */
+  int t0 = fd_wave_min( start );
+  for( int t=t0+(int)(lane>>4); t<FD_OPS_MAX; t+=4 ) {
+    uint64_t gs = sig0 + (lane & 15u);
+    L.ops[t][lane & 15u] = gs < n ? ops[(uint64_t)t*n + gs] : (uint8_t)0;
+  }
+  for( int k=lane; k<8*FD_TAB_ENTRY; k+=64 ) L.tab[FD_QSIGS][k] = fd_gpu_bi_tab[k];
+
+  /* per-lane constant masks */
+  uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
+  uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
+
+  /* Ai = {A,3A,...,15A} cached (avx/fd_ed25519_ge.c:423-481), as fd_k_dsm */
+  fe one; fd_fe_set( one, 1 );
+  fe d111 = q==3u ? FD_GPU_D2 : one;
+  int32_t * tab_s = L.tab[ls];
+  fe vu, vt, f, g;
+  fd_fe_mul( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
+  fd_q_tab_store( tab_s + q*FD_TAB_LANE, vu );
+  {  /* v_p2_dbl: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)), squarings as f*f, Z*(2Z) */
+    fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      f.v[k] = (int32_t)((uint32_t)a.v[k] + ((uint32_t)b.v[k] & mq0));
+      g.v[k] = (int32_t)((uint32_t)f.v[k] << (q==3u ? 1 : 0));
+    }
+    fd_fe_mul( vt, f, g );
+    fd_q_dblmix( vt, m03, s02 );
+  }
+  fd_fe_qperm<FD_QP(3,2,3,1)>( f, vt ); fd_fe_qperm<FD_QP(2,1,0,0)>( g, vt );
+  fd_fe_mul( r, f, g ); fd_q_subadd12( r, m12, mq1 );
+  for( int e=0; e<7; e++ ) {
+    fd_fe_mul( vt, r, vu );
+    fd_q_submix( vt, q >> 1, (q & 1u) ? 0u : ~0u );
+    fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
+    fd_fe_mul( vt, f, g );
+    fd_fe_mul( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
+    fd_q_tab_store( tab_s + (e+1)*FD_TAB_ENTRY + q*FD_TAB_LANE, vu );
+  }
+  __syncthreads();
+
+  /* main loop: the uniform kernel's step (see fd_k_dsm) with lane q of
+     the quad forming product q of the p1p1 -> p3 conversion
+     [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
+     (P, Q, R, S), followed by the op's output mix */
+  fd_fe_set( vt, q ? 1 : 0 );
+  for( int t=t0; t<FD_OPS_MAX; t++ ) {
+    int op = t >= start ? (int)L.ops[t][ls] : 0;
+    uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
+    uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
+    /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
+    uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
+    int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
+    int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
+
+    fe C;
+    fd_fe_qperm<FD_QP(2,1,0,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
+    fd_fe_mul( C, f, g );
+
+    /* f: q0 X+Y, q1 Z, q2 Y (A: Y-X), q3 X (A: T); g: D f (q1 2Z), A E */
+    fe u, w;
+    fd_fe_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fe_qperm<FD_QP(2,2,2,2)>( w, C );
+    uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
+    uint32_t gs = (q==1u && !add) ? 1u : 0u;
+    int32_t E[10] = { ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y };
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_qterm( (uint32_t)w.v[k], mW, mq2 ) );
+      f.v[k] = (int32_t)fk;
+      g.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
+    }
+    fe h; fd_fe_mul( h, f, g );
+
+    /* out = cP P + cQ Q + cR R + cS S, per lane and op kind:
+         q0 D: P-R-S      A: P-R
+         q1 D: R+S        A: P+R
+         q2 D: R-S        A: 2Q-S (positive digit: 2Q+S)
+         q3 D: Q-R+S      A: 2Q+S (positive digit: 2Q-S) */
+    uint32_t pos = add & ~neg;
+    uint32_t mP = mq0 | (mq1 & add);
+    uint32_t mQ = mq3 | (mq2 & add), qs = add ? 1u : 0u;
+    uint32_t mR = mq0 | mq1 | ~add, sR = mq0 | (mq3 & ~add);
+    uint32_t mS = ~((mq0 | mq1) & add), sS = (mq0 & ~add) | (mq2 & ~pos) | (mq3 & pos);
+    uint32_t cadd = (sR & 1u) + (sS & 1u);
+    fe P, Q, R, S;
+    fd_fe_qperm<FD_QP(0,0,0,0)>( P, h ); fd_fe_qperm<FD_QP(1,1,1,1)>( Q, h );
+    fd_fe_qperm<FD_QP(2,2,2,2)>( R, h ); fd_fe_qperm<FD_QP(3,3,3,3)>( S, h );
+#pragma unroll
+    for( int k=0; k<10; k++ )
+      vt.v[k] = (int32_t)(((uint32_t)P.v[k] & mP) + (((uint32_t)Q.v[k] & mQ) << qs)
+                          + (((uint32_t)R.v[k] & mR) ^ sR) + (((uint32_t)S.v[k] & mS) ^ sS) + cadd);
+  }
+
+  /* final p1p1 -> p2: q0 X = t0 t3, q1 Y = t1 t2, q2 Z = t2 t3; then
+     q0 Z r.x, q1 Z r.y and the limb compare (Q2) */
+  fe P2;
+  fd_fe_qperm<FD_QP(0,1,2,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
+  fd_fe_mul( P2, f, g );
+  fd_fe_qperm<FD_QP(2,2,2,2)>( f, P2 );
+  fe cz; fd_fe_mul( cz, f, rr );
+  int eq = 1;
+#pragma unroll
+  for( int k=0; k<8; k++ ) eq &= (cz.v[k] == P2.v[k]);
+  int eq1 = fd_qperm<FD_QP(1,1,1,1)>( eq );
+  if( code == FD_ST_PENDING ) code = (eq & eq1) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if( live && q == 0u ) out[i] = code;
+}
+
+/* ------------------------------------------------------------------ */
 /* Kernel 3 as a signature pool (fd_k_dsm_setup -> fd_k_dsm_pool ->
    fd_k_dsm_final).  The uniform step above pays for both op kinds on
    every lane.  Here each wave owns a pool of FD_POOL signatures whose p1p1
@@ -880,7 +1081,7 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
 
 extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                    hipEvent_t const * ev, int mode, uint64_t pool_min ) {
+                                                    hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   unsigned nb  = (unsigned)((n + 255) / 256);
@@ -901,6 +1102,11 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
                         w->tab, w->pts, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable );
+  } else if( !portable && n <= quad_max ) {
+    if( ev ) hipEventRecord( ev[3], stream );
+    hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
+                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out );
+    if( ev ) hipEventRecord( ev[4], stream );
   } else {
     if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
@@ -913,6 +1119,6 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
 
 extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                               fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
-                                              uint64_t pool_min ) {
-  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode, pool_min );
+                                              uint64_t pool_min, uint64_t quad_max ) {
+  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode, pool_min, quad_max );
 }

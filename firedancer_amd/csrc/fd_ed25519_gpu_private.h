@@ -42,14 +42,16 @@ extern "C" {
 hipError_t fd_ed25519_gpu_upload_tables( void );
 hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                         fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                        hipEvent_t const * ev, int mode, uint64_t pool_min );
+                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
 hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                          void * out, int is384, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
-                                  uint64_t pool_min );
+                                  uint64_t pool_min, uint64_t quad_max );
 /* batches of at least this many signatures take the pooled DSM */
 #define FD_DSM_POOL_MIN_DEFAULT (262144UL)
+/* smaller batches of at most this many signatures take the quad-lane DSM */
+#define FD_DSM_QUAD_MAX_DEFAULT (32768UL)
 #ifdef __cplusplus
 }
 #endif

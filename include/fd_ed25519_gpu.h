@@ -183,6 +183,14 @@ int fd_ed25519_gpu_mode    ( fd_ed25519_gpu_t const * gpu );
 int           fd_ed25519_gpu_set_dsm_pool_min( fd_ed25519_gpu_t * gpu, unsigned long pool_min );
 unsigned long fd_ed25519_gpu_dsm_pool_min    ( fd_ed25519_gpu_t const * gpu );
 
+/* Batches below pool_min of at most quad_max signatures (default 32768;
+   AVX mode) run the DSM with four lanes per signature, lane q carrying
+   the reference's AVX lane q: a quarter of the serial work per lane, the
+   latency schedule for single 4096-signature batches.  Results are
+   identical to the other schedules.  0 = never. */
+int           fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * gpu, unsigned long quad_max );
+unsigned long fd_ed25519_gpu_dsm_quad_max    ( fd_ed25519_gpu_t const * gpu );
+
 /* Zero-copy staging: lend the pinned blob (max_blob + 64 bytes) and
    descriptor (max_sigs) buffers of a free ring slot.  The caller builds
    the batch in place and passes the same pointers to

@@ -205,8 +205,53 @@ def test_pooled_equals_uniform(engine, pooled, n):
     b = base.tile(int(np.ceil(n / len(base))))
     b.desc = b.desc[:n]
     engine.dsm_pool_min = 1 << 62
+    engine.dsm_quad_max = 0
     a = engine.verify_packed(b.blob, b.desc)
     p = pooled.verify_packed(b.blob, b.desc)
     assert (a == p).all(), np.nonzero(a != p)[0][:10]
     assert engine.dsm_pool_min == 1 << 62
     engine.dsm_pool_min = 262144
+    engine.dsm_quad_max = 32768
+
+
+@pytest.fixture(scope="module")
+def uniform():
+    """an engine that runs the one-lane-per-signature DSM (fd_k_dsm) for
+    every batch"""
+    e = fa.Engine(0, 1 << 18, 1 << 28)
+    e.dsm_pool_min = 1 << 62
+    e.dsm_quad_max = 0
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
+def test_uniform_dsm_golden_corpora(uniform, name):
+    b, exp = load_corpus(name)
+    got = uniform.verify_packed(b.blob, b.desc)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("n", [1, 15, 17, 4096 + 77, 30000])
+def test_quad_equals_uniform(engine, uniform, n):
+    """the quad-lane DSM (fd_k_dsm_quad, the default up to 32768
+    signatures) against the uniform one on ragged batches (n not a multiple
+    of the 16 signatures of a wave) of mixed valid / invalid signatures"""
+    base, _ = load_corpus("adversarial")
+    b = base.tile(int(np.ceil(n / len(base))))
+    b.desc = b.desc[:n]
+    assert engine.dsm_quad_max >= n
+    q = engine.verify_packed(b.blob, b.desc)
+    u = uniform.verify_packed(b.blob, b.desc)
+    assert (q == u).all(), np.nonzero(q != u)[0][:10]
+
+
+def test_quad_q2_vectors(engine):
+    """the reference-quirk (Q2) and RFC 8032 vectors through the quad
+    schedule explicitly"""
+    vs = ed_vectors()
+    b = corpus.from_triples([(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in vs])
+    assert len(b) <= engine.dsm_quad_max
+    got = engine.verify_packed(b.blob, b.desc)
+    assert got.tolist() == [v["expected"] for v in vs]
