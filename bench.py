@@ -92,7 +92,7 @@ def parse():
     ap.add_argument("--unique", type=int, default=UNIQUE_SIGS)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--latency-batches", type=int, default=300)
+    ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
@@ -311,6 +311,8 @@ def latency(eng, base, nb):
     lat = np.array(lat[depth:]) * 1e3  # drop the ramp
     return {"batch_sigs": BATCH_SIGS, "batches": nb, "pipeline_depth": depth,
             "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
+            "dsm_schedule": "quad" if 0 < BATCH_SIGS <= eng.dsm_quad_max and BATCH_SIGS < eng.dsm_pool_min else "uniform",
             "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall}
 
 

@@ -27,6 +27,7 @@ ERR_GPU = -17
 
 MODE_AVX = 0        # reference AVX2 build semantics (default)
 MODE_PORTABLE = 1   # reference FD_HAS_AVX=0 build semantics
+MODE_STRICT = 2     # AVX checks with Q1-Q3 fixed (no reference build)
 
 DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"), ("msg_sz", "<u4")])
 

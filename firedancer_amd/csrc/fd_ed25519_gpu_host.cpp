@@ -163,7 +163,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
 
 extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
-  if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE) ) return FD_ED25519_ERR_ARG;
+  if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE && mode != FD_ED25519_GPU_MODE_STRICT) ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   g->mode = mode;
   return 0;

@@ -107,7 +107,7 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 
 extern "C" __global__ void __launch_bounds__(256, 4)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start ) {
+           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
@@ -123,8 +123,9 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t 
   int st = FD_ST_PENDING;
   if( s31 > 0x10u ) st = FD_ED25519_ERR_SIG;
   else if( s31 == 0x10u ) {
-    /* s[16..30] nonzero -> early SUCCESS (Q1, fd_ed25519_user.c:379) */
-    if( sw[4] | sw[5] | sw[6] | (sw[7] & 0x00ffffffu) ) st = FD_ED25519_SUCCESS;
+    /* s[16..30] nonzero -> early SUCCESS (Q1, fd_ed25519_user.c:379);
+       strict mode: S > L, ERR_SIG */
+    if( sw[4] | sw[5] | sw[6] | (sw[7] & 0x00ffffffu) ) st = strict ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
     else {
       /* compare s[0..15] against l_low (little endian 128-bit): S >= L -> ERR_SIG */
       uint64_t lo = ((uint64_t)sw[1] << 32) | sw[0], hi = ((uint64_t)sw[3] << 32) | sw[2];
@@ -193,6 +194,15 @@ FD_DEV void fd_small_dbl( fe (&r)[4], fe const & X, fe const & Y, fe const & Z )
   fd_fe_sub( r[3], r[3], r[2] );
 }
 
+/* field-value equality (canonical forms), the strict mode's compare */
+FD_DEV int fd_fe_value_eq( fe const & a, fe const & b ) {
+  int32_t ca[10], cb[10]; fd_fe_canon( ca, a ); fd_fe_canon( cb, b );
+  int eq = 1;
+#pragma unroll
+  for( int i=0; i<10; i++ ) eq &= (ca[i] == cb[i]);
+  return eq;
+}
+
 FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
   int eq = 1;
 #pragma unroll
@@ -203,7 +213,7 @@ FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
              int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
-             int portable ) {
+             int portable, int strict ) {
   /* portable mode (ref/fd_ed25519_ge.c:242-288 via fd_ed25519_user.c:
      400-403 with 2POINT 0): only A is decompressed (the grid covers
      j < n) and there is no small-order test */
@@ -238,6 +248,13 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
     fd_fe_add( check, vxx, u );
     if( fd_fe_isnonzero( check ) ) bad = 1;
     else fd_fe_mul_scalar( x, x, FD_GPU_SQRTM1 );
+  }
+  if( strict ) {
+    /* strict mode (RFC 8032 section 5.1.3): y >= p or x = 0 with the
+       sign bit set fail decoding (the reference accepts both, Q3) */
+    uint32_t all1 = w[1] & w[2] & w[3] & w[4] & w[5] & w[6];
+    if( (w[7] & 0x7fffffffu) == 0x7fffffffu && all1 == 0xffffffffu && w[0] >= 0xffffffedu ) bad = 1;
+    if( !bad && (w[7] >> 31) && !fd_fe_isnonzero( x ) ) bad = 1;
   }
   if( bad ) { pstat[j] = FD_PT_BAD; return; }
   if( fd_fe_isnegative( x ) != (int)(w[7] >> 31) ) fd_fe_neg( x, x );
@@ -326,7 +343,7 @@ extern "C" __global__ void __launch_bounds__(256, FD_DSM_WAVES)
 fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
           int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
           int32_t * __restrict__ tab, int32_t * __restrict__ out,
-          uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable ) {
+          uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable, int strict ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   /* lanes past n stay in the wave (the step loop is wave-uniform) but
      read item 0 and store nothing */
@@ -513,6 +530,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   int eq = 1;
 #pragma unroll
   for( int k=0; k<8; k++ ) eq &= (xz.v[k] == X.v[k]) & (yz.v[k] == Y.v[k]);
+  if( strict ) eq = fd_fe_value_eq( xz, X ) & fd_fe_value_eq( yz, Y );
   if( code == FD_ST_PENDING ) code = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   if( live ) out[i] = code;
 }
@@ -578,7 +596,7 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
 extern "C" __global__ void __launch_bounds__(64)
 fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-               int32_t * __restrict__ out ) {
+               int32_t * __restrict__ out, int strict ) {
   __shared__ __attribute__((aligned(16))) fd_quad_lds L;
   uint32_t lane = threadIdx.x;
   uint32_t q    = lane & 3u, ls = lane >> 2;
@@ -713,6 +731,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   int eq = 1;
 #pragma unroll
   for( int k=0; k<8; k++ ) eq &= (cz.v[k] == P2.v[k]);
+  if( strict ) eq = fd_fe_value_eq( cz, P2 );
   int eq1 = fd_qperm<FD_QP(1,1,1,1)>( eq );
   if( code == FD_ST_PENDING ) code = (eq & eq1) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   if( live && q == 0u ) out[i] = code;
@@ -987,7 +1006,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_dsm_final( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                 int32_t const * __restrict__ pts, int32_t * __restrict__ out,
-                uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable ) {
+                uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable, int strict ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
   uint64_t m = 2*n;
@@ -1035,6 +1054,7 @@ fd_k_dsm_final( uint64_t n, int32_t const * __restrict__ status, int32_t const *
   int eq = 1;
 #pragma unroll
   for( int k=0; k<8; k++ ) eq &= (xz.v[k] == X.v[k]) & (yz.v[k] == Y.v[k]);
+  if( strict ) eq = fd_fe_value_eq( xz, X ) & fd_fe_value_eq( yz, Y );
   out[i] = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
@@ -1084,13 +1104,14 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
                                                     hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
+  int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
   hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
-  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start );
+  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start, strict );
   if( ev ) hipEventRecord( ev[1], stream );
-  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable );
+  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable, strict );
   if( ev ) hipEventRecord( ev[2], stream );
   /* phases 3-5: DSM setup (Ai tables), DSM main loop, final compare; the
      uniform schedule is one kernel (its time lands in phase 4) */
@@ -1101,16 +1122,16 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
     hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
                         w->tab, w->pts, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
-    hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable );
+    hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
   } else if( !portable && n <= quad_max ) {
     if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
-                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out );
+                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
     if( ev ) hipEventRecord( ev[4], stream );
   } else {
     if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
-                        blob, desc, portable );
+                        blob, desc, portable, strict );
     if( ev ) hipEventRecord( ev[4], stream );
   }
   if( ev ) hipEventRecord( ev[5], stream );

@@ -167,10 +167,17 @@ fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
      FD_ED25519_GPU_MODE_PORTABLE: the FD_HAS_AVX=0 build: A-only
        decompression (R off-curve is ERR_MSG, not ERR_PUBKEY), no
        small-order tests, canonical encoding of R compared with r
-       (fd_ed25519_user.c:400-431 with FD_ED25519_VERIFY_USE_2POINT 0).
+       (fd_ed25519_user.c:400-431 with FD_ED25519_VERIFY_USE_2POINT 0);
+     FD_ED25519_GPU_MODE_STRICT: no reference build (SURVEY.md section 8f
+       row 4): the AVX mode's checks, order and error codes with the
+       quirks fixed -- S >= L is always ERR_SIG (Q1), non-canonical
+       y >= p and x = 0 with the sign bit set fail decoding with
+       ERR_PUBKEY (Q3, RFC 8032 section 5.1.3), the group equation is
+       compared on field values (Q2).  Never used for parity numbers.
    Applies to batches launched after the call. */
 #define FD_ED25519_GPU_MODE_AVX      (0)
 #define FD_ED25519_GPU_MODE_PORTABLE (1)
+#define FD_ED25519_GPU_MODE_STRICT   (2)
 int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * gpu, int mode );
 int fd_ed25519_gpu_mode    ( fd_ed25519_gpu_t const * gpu );
 

@@ -638,6 +638,72 @@ EXPORT int oracle_verify_portable( void const * msg, u64 sz, void const * sig, v
   return verify_portable( msg, sz, sig, pub );
 }
 
+/* STRICT: not a reference build.  The optional mode of SURVEY.md section
+   8f row 4 that fixes the AVX build's quirks Q1-Q3 and otherwise keeps
+   its checks, order and error codes (Q4, fd_ed25519_user.c:372-427):
+     - S >= L is ERR_SIG for every S (Q1 fixed: no early SUCCESS at
+       fd_ed25519_user.c:379), RFC 8032 section 5.1.7 step 1;
+     - A or R decoding fails (ERR_PUBKEY, Q4's code for a bad point) on a
+       non-canonical y >= p or on x = 0 with the sign bit set (Q3 fixed),
+       RFC 8032 section 5.1.3 steps 1 and 4;
+     - small-order A is ERR_PUBKEY, small-order R ERR_SIG (kept from the
+       AVX build, fd_ed25519_user.c:382-395);
+     - the group equation is compared on field values: canonical
+       encodings of x Z, X and of y Z, Y (Q2 fixed), ERR_MSG.
+   Its parity is against this restatement only ("parity unpinned" with
+   respect to the reference, which has no such build); tests pin it to
+   the AVX oracle on every input none of Q1-Q3 touches and to RFC 8032's
+   vectors, including the Q2 vectors the AVX build rejects. */
+static int s_lt_l( u8 const * s ) {
+  static u8 const L[32] = { 0xED,0xD3,0xF5,0x5C,0x1A,0x63,0x12,0x58,0xD6,0x9C,0xF7,0xA2,0xDE,0xF9,0xDE,0x14,
+                            0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0x10 };
+  for( int i=31; i>=0; i-- ) {
+    if( s[i] < L[i] ) return 1;
+    if( s[i] > L[i] ) return 0;
+  }
+  return 0;
+}
+/* y (bit 255 ignored) < p = 2^255 - 19 */
+static int y_canonical( u8 const * e ) {
+  if( (e[31] & 0x7f) != 0x7f ) return 1;
+  for( int i=30; i>=1; i-- ) if( e[i] != 0xff ) return 1;
+  return e[0] < 0xed;
+}
+static int ge_frombytes_strict( ge_p3 * h, u8 const * e ) {
+  if( !y_canonical( e ) ) return -2;
+  if( ge_frombytes_lane( h, e ) ) return -2;
+  if( (e[31] >> 7) && !fe_isnonzero( &h->X ) ) return -2;
+  return 0;
+}
+
+static int verify_strict( void const * msg, u64 sz, void const * sig, void const * pub ) {
+  u8 const * r = (u8 const *)sig;
+  u8 const * s = r + 32;
+  if( !s_lt_l( s ) ) return -1;
+  ge_p3 A, Rd;
+  if( ge_frombytes_strict( &A,  (u8 const *)pub ) ) return -2;
+  if( ge_frombytes_strict( &Rd, r ) )               return -2;
+  if( ge_is_small_order( &A  ) ) return -2;
+  if( ge_is_small_order( &Rd ) ) return -1;
+  fe_neg( &A.X, &A.X );
+  fe_neg( &A.T, &A.T );
+  u8 h[64];
+  sha512_3( h, r, 32, (u8 const *)pub, 32, (u8 const *)msg, sz );
+  oracle_sc_reduce( h, h );
+  ge_p2 R;
+  ge_dsm( &R, h, &A, s );
+  fe xz, yz;
+  fe_mul_avx( &xz, &R.Z, &Rd.X );
+  fe_mul_avx( &yz, &R.Z, &Rd.Y );
+  u8 a[32], b[32], c[32], d[32];
+  fe_tobytes( a, &xz ); fe_tobytes( b, &R.X ); fe_tobytes( c, &yz ); fe_tobytes( d, &R.Y );
+  return ( memcmp( a, b, 32 ) | memcmp( c, d, 32 ) ) ? -3 : 0;
+}
+
+EXPORT int oracle_verify_strict( void const * msg, u64 sz, void const * sig, void const * pub ) {
+  return verify_strict( msg, sz, sig, pub );
+}
+
 /* ---------------------------------------------------------------- */
 /* Internals exported for differential tests against the reference. */
 
@@ -663,8 +729,9 @@ typedef struct {
 static void * batch_worker( void * arg ) {
   batch_job_t * j = (batch_job_t *)arg;
   for( u64 i=j->lo; i<j->hi; i++ )
-    j->out[i] = j->portable ? verify_portable( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i )
-                            : oracle_verify  ( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i );
+    j->out[i] = j->portable==1 ? verify_portable( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i )
+              : j->portable==2 ? verify_strict  ( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i )
+              :                  oracle_verify  ( j->data + j->msg_off[i], j->msg_sz[i], j->sig + 64*i, j->pub + 32*i );
   return NULL;
 }
 
@@ -689,6 +756,11 @@ EXPORT void oracle_verify_batch( u64 n, u8 const * sig, u8 const * pub, u8 const
 EXPORT void oracle_verify_batch_portable( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
                                           u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
   verify_batch_mode( n, sig, pub, data, msg_off, msg_sz, out, nthreads, 1 );
+}
+
+EXPORT void oracle_verify_batch_strict( u64 n, u8 const * sig, u8 const * pub, u8 const * data,
+                                        u64 const * msg_off, u32 const * msg_sz, i32 * out, int nthreads ) {
+  verify_batch_mode( n, sig, pub, data, msg_off, msg_sz, out, nthreads, 2 );
 }
 
 /* ---------------------------------------------------------------- */
