@@ -876,6 +876,9 @@ FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
    128 slots x 8 B = 20 KiB per wave, 8 waves = the CU's 160 KiB).  Slot s holds signature
    gw + s*nwaves. */
 #define FD_POOL 128
+#ifndef FD_POOL_BISECT
+#define FD_POOL_BISECT 0
+#endif
 struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS accesses (64 banks) */
 
 FD_DEV void fd_pool_ld( fe4 & vt, fd_pool_lds const & L, uint32_t s ) {
@@ -927,6 +930,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   }
   fd_mem_fence();
 
+  int lo_d = 0, lo_a = 0;   /* last selection bound per op kind */
   for(;;) {
     int m0 = mt[0], m1 = mt[1];
     int t0 = m0 >> 8, t1 = m1 >> 8;
@@ -943,6 +947,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       /* the 64 candidates with the smallest t (furthest from the end of
          their streams): lo = largest bound with at most 64 candidates
          below it, ties at lo taken in slot order */
+#if FD_POOL_BISECT
       int lo = 0, hi = FD_OPS_MAX + 1;         /* 10 halvings close 769 (unrolled, branch-free) */
 #pragma unroll
       for( int it=0; it<10; it++ ) {
@@ -952,6 +957,16 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
         lo = ok ? mid : lo;
         hi = ok ? hi : mid;
       }
+#else
+      /* the bound moves little between iterations of one kind: walk it
+         from its last value (c(0) = 0 <= 64 < c(FD_OPS_MAX) = nc) */
+      int lo = kind ? lo_a : lo_d;
+#define FD_CNT_BELOW(b) ((uint32_t)(__popcll( __ballot( c0 && t0 < (b) ) ) + __popcll( __ballot( c1 && t1 < (b) ) )))
+      if( FD_CNT_BELOW( lo ) > 64u ) { do lo--; while( FD_CNT_BELOW( lo ) > 64u ); }
+      else { while( FD_CNT_BELOW( lo + 1 ) <= 64u ) lo++; }
+#undef FD_CNT_BELOW
+      if( kind ) lo_a = lo; else lo_d = lo;
+#endif
       uint64_t y0 = __ballot( c0 && t0 < lo ), y1 = __ballot( c1 && t1 < lo );
       uint64_t z0 = __ballot( c0 && t0 == lo ), z1 = __ballot( c1 && t1 == lo );
       uint32_t need = 64u - (uint32_t)(__popcll( y0 ) + __popcll( y1 ));
