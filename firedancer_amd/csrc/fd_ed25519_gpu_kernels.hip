@@ -850,22 +850,6 @@ FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, int32_t const 
   }
 }
 
-/* index of the r-th (0-based) set bit of x, r < popcount(x): the wave
-   shares x (scalar), lanes ask for different r */
-FD_DEV uint32_t fd_nth_bit( uint64_t x, uint32_t r ) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  uint32_t nlo = (uint32_t)__builtin_popcount( lo );
-  uint32_t w = r < nlo ? lo : hi, base = r < nlo ? 0u : 32u;
-  r = r < nlo ? r : r - nlo;
-  uint32_t pos = 0;
-#pragma unroll
-  for( uint32_t step=16; step; step>>=1 ) {
-    uint32_t below = w & ((1u << (pos + step)) - 1u);   /* pos + step <= 31 */
-    pos += (uint32_t)__builtin_popcount( below ) <= r ? step : 0u;
-  }
-  return base + pos;
-}
-
 FD_DEV uint32_t fd_lanes_below( uint64_t m ) {
   return __builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
 }
@@ -979,14 +963,20 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     }
     uint32_t n0 = (uint32_t)__popcll( x0 );
 
-    /* lane l steps the l-th selected slot (bank-0 slots first) */
-    uint32_t bank = lane >= n0;
-    uint32_t j    = fd_nth_bit( bank ? x1 : x0, bank ? lane - n0 : lane );
+    /* lane l steps the l-th selected slot (bank-0 slots first): the owners
+       push (slot, t, op) forward to their stepping lanes (ds_permute; the
+       other lanes fill the remaining destinations, one lane each) */
+    uint32_t b0 = fd_lanes_below( x0 ), b1 = fd_lanes_below( x1 );
+    uint32_t n1 = nc - n0;
+    uint32_t d0 = ((x0 >> lane) & 1ULL) ? b0 : n0 + (lane - b0);
+    uint32_t q1 = lane - b1;
+    uint32_t d1 = ((x1 >> lane) & 1ULL) ? n0 + b1 : (q1 < n0 ? q1 : q1 + n1);
+    int p0 = __builtin_amdgcn_ds_permute( (int)(d0 << 2), m0 | (int)(lane << 24) );
+    int p1 = __builtin_amdgcn_ds_permute( (int)(d1 << 2), m1 | (int)((lane + 64u) << 24) );
+    int pm = lane < n0 ? p0 : p1;
     int act = lane < nc;
-    j = act ? j : lane;
-    uint32_t s = j + 64u*bank;
-    int ma = __shfl( m0, (int)j, 64 ), mb = __shfl( m1, (int)j, 64 );
-    int mm = bank ? mb : ma;
+    uint32_t s = act ? ((uint32_t)pm >> 24) & 127u : lane;
+    int mm = pm & 0xffffff;
     int nm = mm;
     if( act ) {
       int t = mm >> 8, op = mm & 255;
@@ -1008,7 +998,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     }
     fd_mem_fence();
     /* owners take their stepped slots' new (t, op) from the stepping lanes */
-    int r0 = (int)fd_lanes_below( x0 ), r1 = (int)(n0 + fd_lanes_below( x1 ));
+    int r0 = (int)b0, r1 = (int)(n0 + b1);
     int v0 = __shfl( nm, r0 & 63, 64 ), v1 = __shfl( nm, r1 & 63, 64 );
     if( (x0 >> lane) & 1ULL ) mt[0] = v0;
     if( (x1 >> lane) & 1ULL ) mt[1] = v1;
