@@ -327,10 +327,11 @@ FD_DEV void fd_entry_at( fe & E0, fe & E1, fe & E2, fe & E3, int32_t const * ent
   fd_tab_lane( E2, ent + (neg ? 1 : 2)*FD_TAB_LANE );
   fd_tab_lane( E3, ent + 3*FD_TAB_LANE );
 }
-FD_DEV void fd_entry( fe & E0, fe & E1, fe & E2, fe & E3, int op, int32_t const * tab_i, int32_t const * bi ) {
+FD_DEV void fd_entry( fe & E0, fe & E1, fe & E2, fe & E3, int op, int32_t const * tab_i, uint64_t estride,
+                      int32_t const * bi ) {
   int e = op & 7, neg = (op >> 5) & 1;
   if( op & 0x40 ) fd_entry_at( E0, E1, E2, E3, bi    + e*FD_TAB_ENTRY, neg );
-  else            fd_entry_at( E0, E1, E2, E3, tab_i + e*FD_TAB_ENTRY, neg );
+  else            fd_entry_at( E0, E1, E2, E3, tab_i + (uint64_t)e*estride, neg );
 }
 
 FD_DEV int fd_wave_min( int x ) {
@@ -453,7 +454,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
     }
     /* the table entry is read by add steps only (the Ai table does not fit
        the caches at full batch size, so D steps must not touch it) */
-    if( is_add ) fd_entry( E0, E1, E2, E3, op, tab_i, bi_tab );
+    if( is_add ) fd_entry( E0, E1, E2, E3, op, tab_i, FD_TAB_ENTRY, bi_tab );
     fe h0, h1, h2, h3;   /* P, Q, R, S */
     {
       fe xy, g0, g1;
@@ -754,29 +755,66 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
    results are limb-identical. */
 
 
+/* entry e of the wave's 64 signatures i0.. -> tab[e][i0..][4][12], through
+   the wave's LDS stage (rows past n are not written) */
+FD_QDEV void fd_tab_store_rows( int32_t * tab, uint64_t n, uint64_t i0, int e, fe4 const & v, int4 * st, uint32_t lane ) {
+  int4 * q = st + lane*(FD_TAB_ENTRY/4);
+#pragma unroll
+  for( int l=0; l<4; l++ ) {
+    q[3*l+0] = make_int4( v.l[l].v[0], v.l[l].v[1], v.l[l].v[2], v.l[l].v[3] );
+    q[3*l+1] = make_int4( v.l[l].v[4], v.l[l].v[5], v.l[l].v[6], v.l[l].v[7] );
+    q[3*l+2] = make_int4( v.l[l].v[8], v.l[l].v[9], 0, 0 );
+  }
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "wavefront" );
+  int4 * g = (int4 *)(tab + ((uint64_t)e*n + i0)*FD_TAB_ENTRY);
+  uint64_t lim = (n - i0 < 64u ? n - i0 : 64u) * (FD_TAB_ENTRY/4);   /* int4 rows of live signatures */
+#pragma unroll
+  for( int k=0; k<FD_TAB_ENTRY/4; k++ ) {
+    uint32_t c = lane + 64u*(uint32_t)k;
+    if( c < lim ) g[c] = st[c];
+  }
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "wavefront" );
+}
+
 /* Ai table for one signature: the uniform kernel's precompute
    (avx/fd_ed25519_ge.c:423-481), one lane per signature */
-extern "C" __global__ void __launch_bounds__(256)
+#ifndef FD_SETUP_WAVES
+#define FD_SETUP_WAVES 2
+#endif
+extern "C" __global__ void __launch_bounds__(256, FD_SETUP_WAVES)
 fd_k_dsm_setup( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                 int32_t const * __restrict__ pts, int32_t * __restrict__ tab, int portable ) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= n ) return;
-  if( status[i] != FD_ST_PENDING || pstat[i] != FD_PT_OK || (!portable && pstat[n+i] != FD_PT_OK) ) return;
+  /* table layout [entry][sig][lane 4][12]: a wave's 64 entries e are one
+     12 KiB run, stored through LDS as coalesced 1 KiB rows (a lane's own
+     192-byte entry would touch 64 cache lines per store instruction) */
+  __shared__ __attribute__((aligned(16))) int4 stage[4][64*FD_TAB_ENTRY/4];
+  uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  uint32_t lane = threadIdx.x & 63u;
+  if( i0 >= n ) return;                        /* whole waves only: the store is cooperative */
+  uint64_t i = i0 + lane;
+  uint64_t ii = i < n ? i : i0;
   uint64_t m = 2*n;
+  int4 * st = stage[threadIdx.x >> 6];
   fe4 vr, vt, vu;
 #pragma unroll
   for( int k=0; k<10; k++ ) {
-    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + i]);
-    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + i];
-    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + i];
-    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + i]);
+    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + ii]);
+    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + ii];
+    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + ii];
+    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + ii]);
   }
+  /* non-pending signatures run on their (unused) inputs: their entries are
+     never read */
   fe4 d111;
 #pragma unroll
   for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
   d111.l[3] = FD_GPU_D2;
   v_mul( vu, vr, d111 ); v_subadd_12( vu );
-  fd_tab_store( tab, i, 0, vu );
+  fd_tab_store_rows( tab, n, i0, 0, vu, st, lane );
   v_p2_dbl( vt, vr.l[2], vr.l[1], vr.l[0] );
   {
     fe4 a, b;
@@ -793,7 +831,7 @@ fd_k_dsm_setup( uint64_t n, int32_t const * __restrict__ status, int32_t const *
     b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
     v_mul( vt, a, b );
     v_mul( vu, vt, d111 ); v_subadd_12( vu );
-    fd_tab_store( tab, i, e+1, vu );
+    fd_tab_store_rows( tab, n, i0, e+1, vu, st, lane );
   }
 }
 
@@ -816,10 +854,10 @@ FD_DEV void fd_pool_dbl( fe4 & vt ) {
 
 /* A step: p1p1 -> p3 ([Z,Y,X,T], :506-508) then
    SUB_MIX(MUL(SUBADD_12(p3), E)) with the signed digit's entry E */
-FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, int32_t const * bi ) {
+FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, uint64_t estride, int32_t const * bi ) {
   /* the entry loads go out first: the conversion products hide their latency */
   fe E0, E1, E2, E3;
-  fd_entry( E0, E1, E2, E3, op, tab_i, bi );
+  fd_entry( E0, E1, E2, E3, op, tab_i, estride, bi );
   fe Z, Y, X, T;
   {
     int32_t g3[10], f0[10];
@@ -985,7 +1023,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       int opn = tn < FD_OPS_MAX ? (int)ops[(uint64_t)tn*n + sg] : 0;   /* prefetch */
       fe4 vt;
       fd_pool_ld( vt, L, s );
-      if( kind ) fd_pool_add( vt, op, tab + sg*FD_TAB_SIG, fd_gpu_bi_tab );
+      if( kind ) fd_pool_add( vt, op, tab + sg*FD_TAB_ENTRY, n*FD_TAB_ENTRY, fd_gpu_bi_tab );
       else       fd_pool_dbl( vt );
       if( tn < FD_OPS_MAX ) {
         fd_pool_st( L, s, vt );
