@@ -62,6 +62,15 @@ FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
   return ((uint64_t)__builtin_amdgcn_alignbit( w2, w1, mis * 8u ) << 32) | __builtin_amdgcn_alignbit( w1, w0, mis * 8u );
 }
 
+#ifndef FD_SHA_BARRIER
+#define FD_SHA_BARRIER 1
+#endif
+FD_DEV uint64_t fd_opaque64u( uint64_t x ) {
+#if defined(__HIP_DEVICE_COMPILE__) && FD_SHA_BARRIER
+  asm( "" : "+v"(x) );
+#endif
+  return x;
+}
 #ifndef FD_SHA_B3
 #define FD_SHA_B3 1
 #endif
@@ -82,15 +91,18 @@ FD_DEV uint32_t fd_bitop3_e8( uint32_t x, uint32_t y, uint32_t z ) {
   return (x & y) | (x & z) | (y & z);
 #endif
 }
+/* The halves are joined behind a value barrier: LLVM otherwise turns the
+   disjoint (hi << 32) | lo into an add and splits every 64-bit add of the
+   result into two (zero-extended halves, plus register moves). */
 FD_DEV uint64_t fd_xor3_64( uint64_t x, uint64_t y, uint64_t z ) {
   if( !FD_SHA_B3 ) return x ^ y ^ z;
-  return ((uint64_t)fd_bitop3_96( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
-       | fd_bitop3_96( (uint32_t)x, (uint32_t)y, (uint32_t)z );
+  return fd_opaque64u( ((uint64_t)fd_bitop3_96( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
+                       | fd_bitop3_96( (uint32_t)x, (uint32_t)y, (uint32_t)z ) );
 }
 FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
   if( !FD_SHA_B3 ) return (x&y) ^ (x&z) ^ (y&z);
-  return ((uint64_t)fd_bitop3_e8( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
-       | fd_bitop3_e8( (uint32_t)x, (uint32_t)y, (uint32_t)z );
+  return fd_opaque64u( ((uint64_t)fd_bitop3_e8( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
+                       | fd_bitop3_e8( (uint32_t)x, (uint32_t)y, (uint32_t)z ) );
 }
 
 #ifndef FD_SHA_UNROLL
