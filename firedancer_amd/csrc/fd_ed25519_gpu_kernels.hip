@@ -898,6 +898,9 @@ FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
    128 slots x 8 B = 20 KiB per wave, 8 waves = the CU's 160 KiB).  Slot s holds signature
    gw + s*nwaves. */
 #define FD_POOL 128
+#ifndef FD_POOL_PRIO
+#define FD_POOL_PRIO 0
+#endif
 #ifndef FD_POOL_BISECT
 #define FD_POOL_BISECT 0
 #endif
@@ -954,6 +957,9 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 
   int lo_d = 0, lo_a = 0;   /* last selection bound per op kind */
   for(;;) {
+#if FD_POOL_PRIO
+    __builtin_amdgcn_s_setprio( 2 );          /* bookkeeping: issue ahead of the other wave's step math */
+#endif
     int m0 = mt[0], m1 = mt[1];
     int t0 = m0 >> 8, t1 = m1 >> 8;
     int l0 = t0 < FD_OPS_MAX, l1 = t1 < FD_OPS_MAX;
@@ -1016,6 +1022,9 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     uint32_t s = act ? ((uint32_t)pm >> 24) & 127u : lane;
     int mm = pm & 0xffffff;
     int nm = mm;
+#if FD_POOL_PRIO
+    __builtin_amdgcn_s_setprio( 0 );
+#endif
     if( act ) {
       int t = mm >> 8, op = mm & 255;
       uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
