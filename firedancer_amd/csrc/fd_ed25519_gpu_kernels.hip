@@ -105,11 +105,10 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 
 #include "fd_ed25519_gpu_wnaf.h"
 
-extern "C" __global__ void __launch_bounds__(256, 4)
-fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict ) {
-  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+static __device__ __forceinline__ void
+fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+              int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
+              uint8_t * sha_stage ) {
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
   uint8_t const * R = blob + d.sig_off;
@@ -146,6 +145,13 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t 
 #pragma unroll
   for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
   op_start[i] = fd_recode( sw, kw, ops + i, n );
+}
+
+extern "C" __global__ void __launch_bounds__(256, 4)
+fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict ) {
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
+  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, ops, op_start, strict, sha_stage );
 }
 
 /* ------------------------------------------------------------------ */
@@ -210,18 +216,19 @@ FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
   return eq;
 }
 
-extern "C" __global__ void __launch_bounds__(256)
-fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-             int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
-             int portable, int strict ) {
+/* status may be NULL (fd_k_front: prep runs concurrently, so nothing is
+   skipped; the DSM's code precedence puts a failed S check first anyway) */
+static __device__ __forceinline__ void
+fd_decomp_body( uint64_t j, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+                int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
+                int portable, int strict ) {
   /* portable mode (ref/fd_ed25519_ge.c:242-288 via fd_ed25519_user.c:
      400-403 with 2POINT 0): only A is decompressed (the grid covers
      j < n) and there is no small-order test */
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t m = 2*n;
   if( j >= (portable ? n : m) ) return;
   uint64_t i = j < n ? j : j - n;
-  if( status[i] != FD_ST_PENDING ) { pstat[j] = FD_PT_OK; return; }
+  if( status && status[i] != FD_ST_PENDING ) { pstat[j] = FD_PT_OK; return; }
   fd_ed25519_gpu_desc_t d = desc[i];
   uint8_t const * s = blob + (j < n ? d.pub_off : d.sig_off);
   uint32_t w[8]; fd_ld32( w, s );
@@ -288,6 +295,29 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
   fd_fe_mul_scalar( c0, tY, one ); fd_fe_mul_scalar( c1, one, tZ );
   int iy = fd_limbs_eq( c0, c1 );
   pstat[j] = (ix & iy) ? FD_PT_SMALL : FD_PT_OK;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+             int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
+             int portable, int strict ) {
+  fd_decomp_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, pstat, pts, portable, strict );
+}
+
+/* Latency front end (batches on the quad schedule): prep and decomp have
+   no data dependence once decomp stops skipping failed S checks, so one
+   launch runs both side by side -- blocks [0, nb_prep) prep, the rest
+   decomp -- and a small batch's front end takes max(prep, decomp)
+   instead of their sum. */
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
+            int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
+  if( blockIdx.x < nb_prep )
+    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, ops, op_start, strict, sha_stage );
+  else
+    fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, desc, NULL, pstat, pts, portable, strict );
 }
 
 /* ------------------------------------------------------------------ */
@@ -1161,9 +1191,17 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
   hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
-  hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start, strict );
-  if( ev ) hipEventRecord( ev[1], stream );
-  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable, strict );
+  int quad = n < pool_min && !portable && n <= quad_max;
+  if( quad ) {
+    /* latency path: prep and decomp in one launch (their time lands in phase 1) */
+    hipLaunchKernelGGL( fd_k_front, dim3(nb + nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start,
+                        w->pstat, w->pts, portable, strict, nb );
+    if( ev ) hipEventRecord( ev[1], stream );
+  } else {
+    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start, strict );
+    if( ev ) hipEventRecord( ev[1], stream );
+    hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable, strict );
+  }
   if( ev ) hipEventRecord( ev[2], stream );
   /* phases 3-5: DSM setup (Ai tables), DSM main loop, final compare; the
      uniform schedule is one kernel (its time lands in phase 4) */
@@ -1175,7 +1213,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
                         w->tab, w->pts, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
-  } else if( !portable && n <= quad_max ) {
+  } else if( quad ) {
     if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
                         n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
