@@ -267,6 +267,8 @@ def main():
         }
         if not a.no_latency:
             res["latency"] = latency(eng, base, a.latency_batches)
+            # one batch in flight at a time: the per-batch floor
+            res["latency"]["depth1"] = latency(eng, base, max(a.latency_batches // 5, 20), depth=1)
         if not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, min(16, os.cpu_count() or 8))
         res["corpus_gen_s"] = gen_s
@@ -277,11 +279,12 @@ def main():
         dist.destroy_process_group()
 
 
-def latency(eng, base, nb):
+def latency(eng, base, nb, depth=None):
     """Single 4096-signature batches, host pinned ring -> GPU -> host,
-    depth-deep pipeline kept full; submit -> completion per batch."""
+    depth-deep pipeline kept full (default: every ring slot); submit ->
+    completion per batch."""
     nb = max(nb, 20)
-    depth = eng.depth
+    depth = min(depth or eng.depth, eng.depth)
     starts = np.random.default_rng(7).integers(0, len(base) - BATCH_SIGS, nb)
     # each batch: its own compacted blob (the txn payload bytes it references)
     jobs = []
