@@ -931,9 +931,6 @@ FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
 #ifndef FD_POOL_PRIO
 #define FD_POOL_PRIO 0
 #endif
-#ifndef FD_POOL_BISECT
-#define FD_POOL_BISECT 0
-#endif
 struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS accesses (64 banks) */
 
 FD_DEV void fd_pool_ld( fe4 & vt, fd_pool_lds const & L, uint32_t s ) {
@@ -994,39 +991,40 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     int t0 = m0 >> 8, t1 = m1 >> 8;
     int l0 = t0 < FD_OPS_MAX, l1 = t1 < FD_OPS_MAX;
     int a0 = l0 && (m0 & FD_OP_ADD), a1 = l1 && (m1 & FD_OP_ADD);
-    uint32_t nA = (uint32_t)(__popcll( __ballot( a0 ) ) + __popcll( __ballot( a1 ) ));
-    uint32_t nL = (uint32_t)(__popcll( __ballot( l0 ) ) + __popcll( __ballot( l1 ) ));
+    uint64_t A0 = __ballot( a0 ), A1 = __ballot( a1 ), L0 = __ballot( l0 ), L1 = __ballot( l1 );
+    uint32_t nA = (uint32_t)(__popcll( A0 ) + __popcll( A1 ));
+    uint32_t nL = (uint32_t)(__popcll( L0 ) + __popcll( L1 ));
     if( !nL ) break;
     int kind = nA >= 64u || nA == nL;          /* 1: additions, 0: doublings */
-    int c0 = kind ? a0 : (l0 && !a0), c1 = kind ? a1 : (l1 && !a1);
-    uint64_t x0 = __ballot( c0 ), x1 = __ballot( c1 );
+    uint64_t x0 = kind ? A0 : (L0 & ~A0), x1 = kind ? A1 : (L1 & ~A1);   /* candidates */
     uint32_t nc = (uint32_t)(__popcll( x0 ) + __popcll( x1 ));
     if( nc > 64u ) {
       /* the 64 candidates with the smallest t (furthest from the end of
          their streams): lo = largest bound with at most 64 candidates
-         below it, ties at lo taken in slot order */
-#if FD_POOL_BISECT
-      int lo = 0, hi = FD_OPS_MAX + 1;         /* 10 halvings close 769 (unrolled, branch-free) */
-#pragma unroll
-      for( int it=0; it<10; it++ ) {
-        int mid = (lo + hi) >> 1;
-        uint32_t c = (uint32_t)(__popcll( __ballot( c0 && t0 < mid ) ) + __popcll( __ballot( c1 && t1 < mid ) ));
-        int ok = c <= 64u;
-        lo = ok ? mid : lo;
-        hi = ok ? hi : mid;
-      }
-#else
-      /* the bound moves little between iterations of one kind: walk it
-         from its last value (c(0) = 0 <= 64 < c(FD_OPS_MAX) = nc) */
+         below it, ties at lo taken in slot order.  The bound moves little
+         between iterations of one kind, so it is walked from its last
+         value (M(0) is empty, M(FD_OPS_MAX) holds all nc > 64); the walk's
+         own probes give the masks below lo (y) and at lo (z). */
+#define FD_BELOW( x, t, b ) ( (x) & __ballot( (t) < (b) ) )
+#define FD_CNT( u, v )      ( (uint32_t)(__popcll( u ) + __popcll( v )) )
       int lo = kind ? lo_a : lo_d;
-#define FD_CNT_BELOW(b) ((uint32_t)(__popcll( __ballot( c0 && t0 < (b) ) ) + __popcll( __ballot( c1 && t1 < (b) ) )))
-      if( FD_CNT_BELOW( lo ) > 64u ) { do lo--; while( FD_CNT_BELOW( lo ) > 64u ); }
-      else { while( FD_CNT_BELOW( lo + 1 ) <= 64u ) lo++; }
-#undef FD_CNT_BELOW
+      uint64_t y0 = FD_BELOW( x0, t0, lo ), y1 = FD_BELOW( x1, t1, lo ), z0, z1;
+      if( FD_CNT( y0, y1 ) > 64u ) {
+        do {
+          z0 = y0; z1 = y1; lo--;
+          y0 = FD_BELOW( x0, t0, lo ); y1 = FD_BELOW( x1, t1, lo );
+        } while( FD_CNT( y0, y1 ) > 64u );
+      } else {
+        for(;;) {
+          uint64_t u0 = FD_BELOW( x0, t0, lo + 1 ), u1 = FD_BELOW( x1, t1, lo + 1 );
+          if( FD_CNT( u0, u1 ) > 64u ) { z0 = u0; z1 = u1; break; }
+          lo++; y0 = u0; y1 = u1;
+        }
+      }
+#undef FD_BELOW
+#undef FD_CNT
       if( kind ) lo_a = lo; else lo_d = lo;
-#endif
-      uint64_t y0 = __ballot( c0 && t0 < lo ), y1 = __ballot( c1 && t1 < lo );
-      uint64_t z0 = __ballot( c0 && t0 == lo ), z1 = __ballot( c1 && t1 == lo );
+      z0 &= ~y0; z1 &= ~y1;                    /* candidates with t == lo */
       uint32_t need = 64u - (uint32_t)(__popcll( y0 ) + __popcll( y1 ));
       uint32_t nz0 = (uint32_t)__popcll( z0 );
       int k0 = ((z0 >> lane) & 1ULL) && fd_lanes_below( z0 ) < need;
