@@ -142,10 +142,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # rehearsal only (FD_BENCH_SHARE_GPU=1): more ranks than GPUs share them,
+    # with gloo carrying the barrier and the max-over-ranks
+    share = os.environ.get("FD_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = local % max(1, torch.cuda.device_count())
+    red_dev = "cpu" if share else torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
 
@@ -185,10 +194,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], device=dev)
+        okt = torch.tensor([1 if ok else 0], device=red_dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
