@@ -105,9 +105,27 @@ FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
                        | fd_bitop3_e8( (uint32_t)x, (uint32_t)y, (uint32_t)z ) );
 }
 
+#ifndef FD_SHA_ASSOC
+#define FD_SHA_ASSOC 1
+#endif
 #ifndef FD_SHA_UNROLL
 #define FD_SHA_UNROLL 0
 #endif
+/* The adds are grouped so the chain from e (and a) to the next round is
+   short: h + K + W does not depend on this round's e, S0 + maj is formed
+   beside T1; the barriers keep LLVM from re-linearizing the sums. */
+#if FD_SHA_ASSOC
+#define FD_SHA_ROUND(j,kt) do {                                                   \
+    uint64_t hkw = fd_opaque64u( h + (kt) + w[j] );                             \
+    uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
+    uint64_t ch = (e&f) ^ (~e&g);                                               \
+    uint64_t t1 = fd_opaque64u( hkw + ch ) + S1;                                \
+    uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
+    uint64_t mj = fd_maj64( a, b, c );                                          \
+    uint64_t t2 = fd_opaque64u( S0 + mj );                                      \
+    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+t2;                              \
+  } while(0)
+#else
 #define FD_SHA_ROUND(j,kt) do {                                                   \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
     uint64_t ch = (e&f) ^ (~e&g);                                               \
@@ -116,6 +134,7 @@ FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
     uint64_t mj = fd_maj64( a, b, c );                                          \
     h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;                           \
   } while(0)
+#endif
 
 /* 80 rounds as 16 + 4 x 16 so every index into the 16-word schedule
    ring is a compile-time constant (no dynamic register indexing). */
