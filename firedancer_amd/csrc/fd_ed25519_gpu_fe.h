@@ -341,6 +341,33 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
   fd_fe_mul_pre( h, f, f2, g, g19 );
 }
 
+/* h = f*g for a lone wave (the latency kernel): all ten column sums as
+   independent chains, term I of every column before term I+1, then the
+   reference's carry chain on the biased sums (fd_fe_carry).  More
+   instructions than the absorbed chain, but no MAC waits on the MAC
+   before it, which is what a wave with no neighbour on its SIMD pays. */
+template<int I>
+FD_DEV void fd_ilp_terms( fd_mul_cols const & c, int64_t (&S)[10] ) {
+  S[0] = c.template term<0,I>( S[0] ); S[1] = c.template term<1,I>( S[1] );
+  S[2] = c.template term<2,I>( S[2] ); S[3] = c.template term<3,I>( S[3] );
+  S[4] = c.template term<4,I>( S[4] ); S[5] = c.template term<5,I>( S[5] );
+  S[6] = c.template term<6,I>( S[6] ); S[7] = c.template term<7,I>( S[7] );
+  S[8] = c.template term<8,I>( S[8] ); S[9] = c.template term<9,I>( S[9] );
+}
+FD_DEV void fd_fe_mul_ilp( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const & g ) {
+  int32_t f2[10], g19[10];
+  fd_fe_pre_f( f2, f );
+  fd_fe_pre_g( g19, g );
+  fd_mul_cols c = { f.v, f2, g.v, g19 };
+  int64_t S[10];
+#pragma unroll
+  for( int k=0; k<10; k++ ) S[k] = fd_opaque64( FD_BIAS(k) );
+  fd_ilp_terms<0>( c, S ); fd_ilp_terms<1>( c, S ); fd_ilp_terms<2>( c, S ); fd_ilp_terms<3>( c, S );
+  fd_ilp_terms<4>( c, S ); fd_ilp_terms<5>( c, S ); fd_ilp_terms<6>( c, S ); fd_ilp_terms<7>( c, S );
+  fd_ilp_terms<8>( c, S ); fd_ilp_terms<9>( c, S );
+  fd_fe_carry( h, S );
+}
+
 /* ha = fa*ga and hb = fb*gb, interleaved (fd_mul_cols2) */
 FD_DEV void fd_fe_mul2_pre( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int32_t const (&fa2)[10], fd_gpu_fe_t const & ga, int32_t const (&ga19)[10],
                             fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int32_t const (&fb2)[10], fd_gpu_fe_t const & gb, int32_t const (&gb19)[10] ) {

@@ -624,6 +624,20 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   q[2] = make_int4( v.v[8], v.v[9], 0, 0 );
 }
 
+#ifndef FD_QUAD_ILP
+#define FD_QUAD_ILP 0
+#endif
+/* products of the latency kernel.  FD_QUAD_ILP 1 = independent column
+   chains (fd_fe_mul_ilp): measured equal (quad DSM 0.441 ms either way at
+   4,096 signatures) -- a lone wave issues about one instruction per 4-5
+   cycles whatever its ILP, so its latency follows its instruction count,
+   and the absorbed chain has fewer instructions. */
+#if FD_QUAD_ILP
+#define FD_QMUL fd_fe_mul_ilp
+#else
+#define FD_QMUL fd_fe_mul
+#endif
+
 extern "C" __global__ void __launch_bounds__(64)
 fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
@@ -676,7 +690,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   fe d111 = q==3u ? FD_GPU_D2 : one;
   int32_t * tab_s = L.tab[ls];
   fe vu, vt, f, g;
-  fd_fe_mul( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
+  FD_QMUL( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
   fd_q_tab_store( tab_s + q*FD_TAB_LANE, vu );
   {  /* v_p2_dbl: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)), squarings as f*f, Z*(2Z) */
     fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
@@ -685,17 +699,17 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       f.v[k] = (int32_t)((uint32_t)a.v[k] + ((uint32_t)b.v[k] & mq0));
       g.v[k] = (int32_t)((uint32_t)f.v[k] << (q==3u ? 1 : 0));
     }
-    fd_fe_mul( vt, f, g );
+    FD_QMUL( vt, f, g );
     fd_q_dblmix( vt, m03, s02 );
   }
   fd_fe_qperm<FD_QP(3,2,3,1)>( f, vt ); fd_fe_qperm<FD_QP(2,1,0,0)>( g, vt );
-  fd_fe_mul( r, f, g ); fd_q_subadd12( r, m12, mq1 );
+  FD_QMUL( r, f, g ); fd_q_subadd12( r, m12, mq1 );
   for( int e=0; e<7; e++ ) {
-    fd_fe_mul( vt, r, vu );
+    FD_QMUL( vt, r, vu );
     fd_q_submix( vt, q >> 1, (q & 1u) ? 0u : ~0u );
     fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
-    fd_fe_mul( vt, f, g );
-    fd_fe_mul( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
+    FD_QMUL( vt, f, g );
+    FD_QMUL( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
     fd_q_tab_store( tab_s + (e+1)*FD_TAB_ENTRY + q*FD_TAB_LANE, vu );
   }
   __syncthreads();
@@ -716,7 +730,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 
     fe C;
     fd_fe_qperm<FD_QP(2,1,0,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
-    fd_fe_mul( C, f, g );
+    FD_QMUL( C, f, g );
 
     /* f: q0 X+Y, q1 Z, q2 Y (A: Y-X), q3 X (A: T); g: D f (q1 2Z), A E */
     fe u, w;
@@ -730,7 +744,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       f.v[k] = (int32_t)fk;
       g.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
     }
-    fe h; fd_fe_mul( h, f, g );
+    fe h; FD_QMUL( h, f, g );
 
     /* out = cP P + cQ Q + cR R + cS S, per lane and op kind:
          q0 D: P-R-S      A: P-R
@@ -756,9 +770,9 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
      q0 Z r.x, q1 Z r.y and the limb compare (Q2) */
   fe P2;
   fd_fe_qperm<FD_QP(0,1,2,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
-  fd_fe_mul( P2, f, g );
+  FD_QMUL( P2, f, g );
   fd_fe_qperm<FD_QP(2,2,2,2)>( f, P2 );
-  fe cz; fd_fe_mul( cz, f, rr );
+  fe cz; FD_QMUL( cz, f, rr );
   int eq = 1;
 #pragma unroll
   for( int k=0; k<8; k++ ) eq &= (cz.v[k] == P2.v[k]);

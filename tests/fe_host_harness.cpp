@@ -27,6 +27,14 @@ void h_fe_mul( int32_t * h, int32_t const * f, int32_t const * g, unsigned long 
     for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
   }
 }
+void h_fe_mul_ilp( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, b, c;
+    for( int k=0; k<10; k++ ) { a.v[k] = f[10*i+k]; b.v[k] = g[10*i+k]; }
+    fd_fe_mul_ilp( c, a, b );
+    for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
 void h_fe_sqn( int32_t * h, int32_t const * f, int nsq, unsigned long n ) {
   for( unsigned long i=0; i<n; i++ ) {
     fd_gpu_fe_t a, c;

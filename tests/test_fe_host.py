@@ -53,6 +53,11 @@ def test_mul_sqn_vs_reference(harness, ref, bits):
         e = np.zeros(10, np.int32)
         ref.ref_fe_mul_avx(P(e), P(np.ascontiguousarray(F[i])), P(np.ascontiguousarray(G[i])))
         assert (H[i] == e).all(), (bits, i)
+    # the latency kernel's product (independent column chains + the
+    # reference carry chain on biased sums)
+    H2 = np.zeros_like(F)
+    harness.h_fe_mul_ilp(P(H2), P(F), P(G), ctypes.c_ulong(n))
+    assert (H2 == H).all(), bits
     for nsq in (1, 2):
         harness.h_fe_sqn(P(H), P(F), nsq, ctypes.c_ulong(n))
         for i in range(n):
