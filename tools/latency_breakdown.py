@@ -24,10 +24,14 @@ def main():
     if quad is not None:
         eng.dsm_quad_max = int(quad)
     s = torch.cuda.current_stream(dev).cuda_stream
+    pool = os.environ.get("FD_POOL_MIN")
+    if pool is not None:
+        eng.dsm_pool_min = int(pool)
     for n in sizes:
-        d = base.desc[:n].copy()
+        src = base if n <= len(base) else base.tile((n + len(base) - 1) // len(base))
+        d = src.desc[:n].copy()
         hi = int(max((d["msg_off"] + d["msg_sz"]).max(), d["sig_off"].max() + 64))
-        blob = np.ascontiguousarray(base.blob[:hi])
+        blob = np.ascontiguousarray(src.blob[:hi])
         d_blob = torch.from_numpy(np.concatenate([blob, np.zeros(64, np.uint8)])).to(dev)
         d_desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         d_out = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -54,7 +58,7 @@ def main():
             eng.poll(tk, out, block=True)
             lat.append((time.perf_counter() - ts) * 1e3)
         lat = np.array(lat[5:])
-        print(json.dumps({"n": n, "quad_max": eng.dsm_quad_max, "accepted": ok,
+        print(json.dumps({"n": n, "quad_max": eng.dsm_quad_max, "pool_min": eng.dsm_pool_min, "accepted": ok,
                           "kernel_ms_mean": {k: float(v) for k, v in zip(fa.Engine.KERNELS, ks.mean(0))},
                           "kernel_sum_ms": float(ks.sum(1).mean()),
                           "dev_launch_ms": dev_ms,
