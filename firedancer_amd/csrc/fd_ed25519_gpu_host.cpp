@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <mutex>
 #include <atomic>
 #include "fd_ed25519_gpu_private.h"
@@ -24,6 +25,30 @@
 #define FD_GPU_DEPTH_DEFAULT 3
 #define FD_GPU_DEPTH_MAX     8
 #define FD_BLOB_PAD  64UL
+
+/* offset of the descriptors in a slot's staging buffer for a blob of
+   blob_sz bytes */
+/* blocking polls spin this long before sleeping */
+#define FD_POLL_SPIN_NS 20000000L
+
+/* Wait for a slot's completion event: spin on it for up to
+   FD_POLL_SPIN_NS (as a tile busy-polls its rings; hipEventSynchronize's
+   wake-up adds tens of microseconds to a ~0.7 ms batch round trip), then
+   sleep in hipEventSynchronize. */
+static hipError_t fd_event_wait( hipEvent_t ev ) {
+  hipError_t e = hipEventQuery( ev );
+  if( e != hipErrorNotReady ) return e;
+  struct timespec t0, t1;
+  clock_gettime( CLOCK_MONOTONIC, &t0 );
+  for(;;) {
+    __builtin_ia32_pause();
+    if( (e = hipEventQuery( ev )) != hipErrorNotReady ) return e;
+    clock_gettime( CLOCK_MONOTONIC, &t1 );
+    if( (t1.tv_sec - t0.tv_sec) * 1000000000L + (t1.tv_nsec - t0.tv_nsec) > FD_POLL_SPIN_NS ) return hipEventSynchronize( ev );
+  }
+}
+
+static inline unsigned long fd_desc_off( unsigned long blob_sz ) { return (blob_sz + FD_BLOB_PAD + 15UL) & ~15UL; }
 
 struct fd_ed25519_gpu_slot {
   /* pinned host staging */
@@ -114,7 +139,11 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
-  unsigned long blob_cap = max_blob + FD_BLOB_PAD;
+  /* a slot's pinned and device blob buffers also hold the batch's
+     descriptors, 16-aligned after the padded blob, so a batch is ONE H2D
+     copy (a second small copy costs ~17 us of a ~0.75 ms 4096-signature
+     round trip: its own transfer plus the copy-to-copy gap) */
+  unsigned long blob_cap = fd_desc_off( max_blob ) + max_sigs * sizeof(fd_ed25519_gpu_desc_t);
   HIPCHK( hipSetDevice( device ) );
   HIPCHK( fd_ed25519_gpu_upload_tables() );
   for( int s=0; s<g->depth; s++ ) {
@@ -256,22 +285,22 @@ extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_
 static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
                             unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
   if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
-  memset( sl->h_blob + blob_sz, 0, FD_BLOB_PAD );
-  /* out-of-bounds descriptors are replaced by a harmless in-bounds one
-     and reported as FD_ED25519_ERR_ARG after the run */
-  int any_bad = 0;
+  unsigned long doff = fd_desc_off( blob_sz );
+  memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
+  /* descriptors land after the padded blob (one copy); out-of-bounds ones
+     are replaced by a harmless in-bounds one and reported as
+     FD_ED25519_ERR_ARG after the run */
+  fd_ed25519_gpu_desc_t * hd = (fd_ed25519_gpu_desc_t *)(sl->h_blob + doff);
   for( unsigned long i=0; i<n; i++ ) {
     fd_ed25519_gpu_desc_t d = desc[i];
-    if( !fd_desc_ok( &d, blob_sz ) ) { any_bad = 1; d.sig_off = d.pub_off = d.msg_off = 0; d.msg_sz = 0; }
-    sl->h_desc[i] = d;
+    if( !fd_desc_ok( &d, blob_sz ) ) { d.sig_off = d.pub_off = d.msg_off = 0; d.msg_sz = 0; }
+    hd[i] = d;
   }
-  (void)any_bad;
   hipError_t e;
-  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, blob_sz + FD_BLOB_PAD, hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
-    return fd_gpu_fail( "H2D blob", e );
-  if( (e = hipMemcpyAsync( sl->d_desc, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
-    return fd_gpu_fail( "H2D desc", e );
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, sl->d_desc, &sl->work, sl->d_out, sl->stream, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+    return fd_gpu_fail( "H2D blob+desc", e );
+  fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, dd, &sl->work, sl->d_out, sl->stream, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
@@ -297,7 +326,7 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   if( !sl ) return FD_ED25519_ERR_ARG;   /* every slot in flight or lent out */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
-  if( (e = hipEventSynchronize( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+  if( (e = fd_event_wait( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
   fd_slot_collect( sl, blob_sz, desc, out );
   return 0;
 }
@@ -327,7 +356,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
-  hipError_t e = block ? hipEventSynchronize( sl->done ) : hipEventQuery( sl->done );
+  hipError_t e = block ? fd_event_wait( sl->done ) : hipEventQuery( sl->done );
   if( e == hipErrorNotReady ) return 0;
   if( e != hipSuccess ) return fd_gpu_fail( "poll", e );
   std::lock_guard<std::mutex> guard( g->lock );
@@ -432,7 +461,7 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
     if( !cnt ) return FD_ED25519_ERR_ARG;   /* single message larger than the engine's blob */
     int err = fd_slot_enqueue( g, sl, cnt, sl->h_blob, used, sl->h_desc );
     if( err ) return err;
-    if( (e = hipEventSynchronize( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+    if( (e = fd_event_wait( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
     for( unsigned long k=0; k<cnt; k++ ) out[i+k] = sl->h_out[k];
     i += cnt;
   }
