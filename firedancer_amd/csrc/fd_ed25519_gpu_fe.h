@@ -52,7 +52,15 @@ FD_DEV int64_t fd_opaque64( int64_t x ) {
 }
 
 /* m ? a : b bitwise for a lane mask m in {0, ~0} (v_bfi_b32) */
-FD_DEV uint32_t fd_sel( uint32_t m, uint32_t a, uint32_t b ) { return (a & m) | (b & ~m); }
+/* m ? a : b bitwise; v_bitop3_b32 0xCA issues at full rate on gfx950,
+   the v_bfi_b32 LLVM picks for the and/or form at half rate */
+FD_DEV uint32_t fd_sel( uint32_t m, uint32_t a, uint32_t b ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32( m, a, b, 0xCA );
+#else
+  return (a & m) | (b & ~m);
+#endif
+}
 
 FD_DEV int32_t fd_sext26( int64_t x ) { return ((int32_t)((uint32_t)x << 6)) >> 6; }
 FD_DEV int32_t fd_sext25( int64_t x ) { return ((int32_t)((uint32_t)x << 7)) >> 7; }

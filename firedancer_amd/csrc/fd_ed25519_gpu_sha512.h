@@ -94,6 +94,21 @@ FD_DEV uint32_t fd_bitop3_e8( uint32_t x, uint32_t y, uint32_t z ) {
 /* The halves are joined behind a value barrier: LLVM otherwise turns the
    disjoint (hi << 32) | lo into an add and splits every 64-bit add of the
    result into two (zero-extended halves, plus register moves). */
+/* Ch(e,f,g) = e ? f : g as v_bitop3_b32 (table 0xCA, first operand the
+   selector): full rate on gfx950, where the v_bfi_b32 LLVM picks for the
+   and/andn/xor form issues at half rate (profiles/ubench_int_r01.txt) */
+FD_DEV uint32_t fd_bitop3_ca( uint32_t x, uint32_t y, uint32_t z ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32( x, y, z, 0xCA );
+#else
+  return (x & y) | (~x & z);
+#endif
+}
+FD_DEV uint64_t fd_ch64( uint64_t e, uint64_t f, uint64_t g ) {
+  if( !FD_SHA_B3 ) return (e&f) ^ (~e&g);
+  return fd_opaque64u( ((uint64_t)fd_bitop3_ca( (uint32_t)(e>>32), (uint32_t)(f>>32), (uint32_t)(g>>32) ) << 32)
+                       | fd_bitop3_ca( (uint32_t)e, (uint32_t)f, (uint32_t)g ) );
+}
 FD_DEV uint64_t fd_xor3_64( uint64_t x, uint64_t y, uint64_t z ) {
   if( !FD_SHA_B3 ) return x ^ y ^ z;
   return fd_opaque64u( ((uint64_t)fd_bitop3_96( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
@@ -118,7 +133,7 @@ FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
 #define FD_SHA_ROUND(j,kt) do {                                                   \
     uint64_t hkw = fd_opaque64u( h + (kt) + w[j] );                             \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
-    uint64_t ch = (e&f) ^ (~e&g);                                               \
+    uint64_t ch = fd_ch64( e, f, g );                                             \
     uint64_t t1 = fd_opaque64u( hkw + ch ) + S1;                                \
     uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
     uint64_t mj = fd_maj64( a, b, c );                                          \
@@ -128,7 +143,7 @@ FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
 #else
 #define FD_SHA_ROUND(j,kt) do {                                                   \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
-    uint64_t ch = (e&f) ^ (~e&g);                                               \
+    uint64_t ch = fd_ch64( e, f, g );                                             \
     uint64_t t1 = h + S1 + ch + (kt) + w[j];                                    \
     uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
     uint64_t mj = fd_maj64( a, b, c );                                          \

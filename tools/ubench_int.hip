@@ -41,6 +41,19 @@ K_BEGIN(k_dot2_i32_i16) DOT2(c0) DOT2(c1) DOT2(c2) DOT2(c3) DOT2(c4) DOT2(c5) DO
 #define ADDC(c) { unsigned lo=(unsigned)c, hi=(unsigned)(c>>32); asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, 0, vcc" : "+v"(lo), "+v"(hi) : "v"(a) : "vcc"); c = ((uint64_t)hi<<32)|lo; }
 K_BEGIN(k_add_addc) ADDC(c0) ADDC(c1) ADDC(c2) ADDC(c3) ADDC(c4) ADDC(c5) ADDC(c6) ADDC(c7) K_END
 
+// SHA-512 instruction mix (fd_k_prep): 64-bit rotates as v_alignbit_b32
+// pairs, 3-input xor / majority as v_bitop3_b32, Ch as v_bfi_b32
+#define ALIGNBIT(c) { unsigned t=(unsigned)c; asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(t) : "v"(a)); c=t; }
+K_BEGIN(k_alignbit) ALIGNBIT(c0) ALIGNBIT(c1) ALIGNBIT(c2) ALIGNBIT(c3) ALIGNBIT(c4) ALIGNBIT(c5) ALIGNBIT(c6) ALIGNBIT(c7) K_END
+#define BITOP3(c) { unsigned t=(unsigned)c; asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(t) : "v"(a), "v"(b)); c=t; }
+K_BEGIN(k_bitop3) BITOP3(c0) BITOP3(c1) BITOP3(c2) BITOP3(c3) BITOP3(c4) BITOP3(c5) BITOP3(c6) BITOP3(c7) K_END
+#define BFI(c) { unsigned t=(unsigned)c; asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(t) : "v"(a), "v"(b)); c=t; }
+K_BEGIN(k_bfi) BFI(c0) BFI(c1) BFI(c2) BFI(c3) BFI(c4) BFI(c5) BFI(c6) BFI(c7) K_END
+#define XOR32(c) { unsigned t=(unsigned)c; asm volatile("v_xor_b32 %0, %1, %0" : "+v"(t) : "v"(a)); c=t; }
+K_BEGIN(k_xor) XOR32(c0) XOR32(c1) XOR32(c2) XOR32(c3) XOR32(c4) XOR32(c5) XOR32(c6) XOR32(c7) K_END
+#define PERM(c) { unsigned t=(unsigned)c; asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(t) : "v"(a), "v"(b)); c=t; }
+K_BEGIN(k_perm) PERM(c0) PERM(c1) PERM(c2) PERM(c3) PERM(c4) PERM(c5) PERM(c6) PERM(c7) K_END
+
 typedef void (*kfn)(unsigned*, unsigned);
 int main() {
   struct { const char *name; kfn f; int instr_per_op; } ks[] = {
@@ -49,6 +62,8 @@ int main() {
     {"v_mul_hi_i32_i24", k_mul_hi_i32_i24, 1}, {"v_mad_u32_u24", k_mad_u32_u24, 1}, {"v_lshl_add_u64", k_lshl_add_u64, 1},
     {"v_ashrrev_i64", k_ashrrev_i64, 1}, {"v_fma_f64", k_fma_f64, 1}, {"v_dot2_i32_i16", k_dot2_i32_i16, 1},
     {"v_add_co+addc (pair)", k_add_addc, 2},
+    {"v_alignbit_b32", k_alignbit, 1}, {"v_bitop3_b32", k_bitop3, 1}, {"v_bfi_b32", k_bfi, 1},
+    {"v_xor_b32", k_xor, 1}, {"v_perm_b32", k_perm, 1},
   };
   hipDeviceProp_t p; hipGetDeviceProperties(&p, 0);
   int cus = p.multiProcessorCount; double clk = p.clockRate * 1e3;
