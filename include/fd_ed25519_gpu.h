@@ -139,10 +139,12 @@ fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
                            void *                        stream );
 
 /* Asynchronous pipeline over the engine's pinned host rings: submit
-   copies the batch into a free pinned slot and enqueues H2D copy,
-   kernels and D2H copy on that slot's stream; poll returns 1 and fills
-   out when the batch has completed, 0 if still in flight, <0 on error.
-   At most fd_ed25519_gpu_depth() batches may be outstanding. */
+   copies the batch into a free pinned slot (descriptors packed after the
+   padded blob) and enqueues one H2D copy, the kernels and the D2H copy
+   on that slot's stream; poll returns 1 and fills out when the batch has
+   completed, 0 if still in flight, <0 on error (block != 0: spins on the
+   slot's event for up to 20 ms, then sleeps until it completes).  At
+   most fd_ed25519_gpu_depth() batches may be outstanding. */
 int
 fd_ed25519_gpu_submit( fd_ed25519_gpu_t *            gpu,
                        unsigned long                 n,
