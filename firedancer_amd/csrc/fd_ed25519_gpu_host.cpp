@@ -14,6 +14,7 @@
    Nothing here verifies on the CPU: every code comes from the device. */
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -24,6 +25,9 @@
 
 #define FD_GPU_DEPTH_DEFAULT 3
 #define FD_GPU_DEPTH_MAX     8
+#ifndef FD_CU_GROUPS
+#define FD_CU_GROUPS         3   /* CU groups for small ring batches (1: none) */
+#endif
 #define FD_BLOB_PAD  64UL
 
 /* offset of the descriptors in a slot's staging buffer for a blob of
@@ -62,6 +66,7 @@ struct fd_ed25519_gpu_slot {
   fd_ed25519_gpu_work_t   work;
   void *                  d_work_base;
   hipStream_t             stream;
+  hipStream_t             mstream;  /* the slot's CU group (small batches on a ring of depth > 1), or NULL */
   hipEvent_t              done;
   unsigned long           n;
   unsigned long           ticket;   /* 0 = free */
@@ -78,6 +83,7 @@ struct fd_ed25519_gpu {
   int           mode;     /* FD_ED25519_GPU_MODE_* */
   unsigned long pool_min; /* batches >= this take the pooled DSM */
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
+  unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
@@ -161,6 +167,27 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
   }
+  /* CU groups for small ring batches.  A 4,096-signature batch on the
+     latency schedule is lone waves (256 quad-DSM waves, 192 front-end
+     waves); with several in flight, a batch's front end landed on the
+     SIMDs of another batch's quad-DSM waves and ran at their pace (111 ->
+     ~250 us, tools/lat_trace3.py).  Up to FD_CU_GROUPS slots get disjoint
+     CU groups (CU c in group c mod groups, so every group spans all
+     XCDs); batches up to 64 signatures per group CU (one quad wave per
+     SIMD) run there while other ring batches are in flight (A/B, depth 3:
+     p50 0.914 -> 0.80 ms, p99 0.96 -> 0.84 ms), larger ones and lone
+     batches on the whole device. */
+  {
+    int groups = g->depth < FD_CU_GROUPS ? g->depth : FD_CU_GROUPS;
+    int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
+    if( words > 32 ) groups = 1;
+    g->mask_max = groups > 1 ? 64UL * (unsigned long)(ncu / groups) : 0UL;
+    for( int s=0; groups > 1 && s<g->depth; s++ ) {
+      uint32_t mask[32] = { 0 };
+      for( int c=0; c<ncu; c++ ) if( c % groups == s % groups ) mask[c >> 5] |= 1u << (c & 31);
+      HIPCHK( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) );
+    }
+  }
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
   return g;
 fail:
@@ -174,6 +201,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( sl->stream ) hipStreamSynchronize( sl->stream );
+    if( sl->mstream ) { hipStreamSynchronize( sl->mstream ); hipStreamDestroy( sl->mstream ); }
     if( sl->h_blob ) hipHostFree( sl->h_blob );
     if( sl->h_desc ) hipHostFree( sl->h_desc );
     if( sl->h_out  ) hipHostFree( sl->h_out );
@@ -297,14 +325,22 @@ static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsi
     hd[i] = d;
   }
   hipError_t e;
-  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess )
+  /* the slot's CU group only while another ring batch is in flight (a
+     lone batch runs faster spread over the whole device: depth-1 p50
+     0.755 ms there vs 0.80 ms on a third of the CUs) */
+  int others = 0;
+  if( sl->mstream && n <= g->mask_max )
+    for( int s=0; s<g->depth; s++ )
+      if( &g->slot[s] != sl && g->slot[s].ticket && hipEventQuery( g->slot[s].done ) == hipErrorNotReady ) others = 1;
+  hipStream_t st = others ? sl->mstream : sl->stream;
+  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, dd, &sl->work, sl->d_out, sl->stream, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
-  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
+  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
-  if( (e = hipEventRecord( sl->done, sl->stream )) != hipSuccess ) return fd_gpu_fail( "event", e );
+  if( (e = hipEventRecord( sl->done, st )) != hipSuccess ) return fd_gpu_fail( "event", e );
   sl->n = n;
   return 0;
 }

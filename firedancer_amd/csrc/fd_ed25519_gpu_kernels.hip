@@ -308,12 +308,20 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
    no data dependence once decomp stops skipping failed S checks, so one
    launch runs both side by side -- blocks [0, nb_prep) prep, the rest
    decomp -- and a small batch's front end takes max(prep, decomp)
-   instead of their sum. */
-extern "C" __global__ void __launch_bounds__(256)
+   instead of their sum.  One wave per block (FD_FRONT_WAVES 1): with
+   several batches in flight the dispatcher can then put a front-end wave
+   on an idle SIMD; a 4-wave block always puts one of its waves on the
+   SIMD of a resident quad-DSM wave of another batch, and the block (so
+   the front end) ran at that shared SIMD's pace (111 -> 225-280 us,
+   depth-3 trace, tools/lat_trace3.py). */
+#ifndef FD_FRONT_WAVES
+#define FD_FRONT_WAVES 1
+#endif
+extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
 fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
-  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
   if( blockIdx.x < nb_prep )
     fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, ops, op_start, strict, sha_stage );
   else
@@ -1206,8 +1214,10 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   int quad = n < pool_min && !portable && n <= quad_max;
   if( quad ) {
     /* latency path: prep and decomp in one launch (their time lands in phase 1) */
-    hipLaunchKernelGGL( fd_k_front, dim3(nb + nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start,
-                        w->pstat, w->pts, portable, strict, nb );
+    unsigned const bt = 64u*FD_FRONT_WAVES;
+    unsigned const fp = (unsigned)((n + bt - 1) / bt), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
+    hipLaunchKernelGGL( fd_k_front, dim3(fp + fd), dim3(bt), 0, stream, n, blob, desc, w->status, w->ops, w->op_start,
+                        w->pstat, w->pts, portable, strict, fp );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
     hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start, strict );
