@@ -185,7 +185,13 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     for( int s=0; groups > 1 && s<g->depth; s++ ) {
       uint32_t mask[32] = { 0 };
       for( int c=0; c<ncu; c++ ) if( c % groups == s % groups ) mask[c >> 5] |= 1u << (c & 31);
-      HIPCHK( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) );
+      if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess ) {
+        /* no CU masking here: every batch takes the whole device */
+        (void)hipGetLastError();
+        for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
+        g->mask_max = 0UL;
+        break;
+      }
     }
   }
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );

@@ -164,6 +164,32 @@ def test_async_ring(engine):
         assert (out == e).all()
 
 
+def test_ring_cu_groups_vs_reference(engine, oracle):
+    """Small batches kept in flight at full ring depth run on their slots'
+    CU groups (fd_ed25519_gpu_host.cpp): 4 x depth 4096-signature
+    adversarial batches through submit/poll, every code checked against
+    the reference build."""
+    chk = _checker(oracle)
+    b = corpus.adversarial(4096 * 2, 128, seed=99, invalid_frac=0.2)
+    exp = oracle_batch(chk, b)
+    halves = []
+    for h in range(2):
+        d = b.desc[h * 4096:(h + 1) * 4096].copy()
+        halves.append((b.blob, d, exp[h * 4096:(h + 1) * 4096]))
+    inflight = []
+    out = np.zeros(4096, np.int32)
+    for k in range(4 * engine.depth):
+        if len(inflight) == engine.depth:
+            t, e = inflight.pop(0)
+            assert engine.poll(t, out, block=True)
+            assert (out == e).all()
+        blob, d, e = halves[k % 2]
+        inflight.append((engine.submit(blob, d), e))
+    for t, e in inflight:
+        assert engine.poll(t, out, block=True)
+        assert (out == e).all()
+
+
 def test_device_resident(engine):
     """verify_dev on torch-allocated HBM (the bench's path)."""
     torch = pytest.importorskip("torch")
