@@ -170,13 +170,14 @@ def main():
 
     eng = fa.Engine(local, max_sigs=max(n_step, 1 << 16), max_blob=max(len(batch.blob), 1 << 24))
     dev = torch.device("cuda", local)
+    blob_sz = len(batch.blob)
     d_blob = torch.from_numpy(np.concatenate([batch.blob, np.zeros(64, np.uint8)])).to(dev)
     d_desc = torch.from_numpy(batch.desc.view(np.uint8).copy()).to(dev)
     d_out = torch.zeros(n_step, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        eng.verify_dev(n_step, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), stream)
+        eng.verify_dev(n_step, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), stream)
 
     for _ in range(a.warmup):
         step()
@@ -233,7 +234,7 @@ def main():
         reps = max(3, min(a.steps, 10))
         ks = np.zeros(len(fa.Engine.KERNELS))
         for _ in range(reps):
-            ks += eng.verify_dev_timed(n_step, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), stream)
+            ks += eng.verify_dev_timed(n_step, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), stream)
         ks /= reps
         msz = base.desc["msg_sz"].astype(np.int64)
         blocks = float(np.mean([sha_blocks(int(m)) for m in msz]))

@@ -77,9 +77,9 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_delete.restype = None
         L.fd_ed25519_gpu_verify_packed.argtypes = [vp, ul, vp, ul, vp, vp]
         L.fd_ed25519_gpu_verify_packed.restype = ip
-        L.fd_ed25519_gpu_verify_dev.argtypes = [vp, ul, vp, vp, vp, vp]
+        L.fd_ed25519_gpu_verify_dev.argtypes = [vp, ul, vp, ul, vp, vp, vp]
         L.fd_ed25519_gpu_verify_dev.restype = ip
-        L.fd_ed25519_gpu_verify_dev_timed.argtypes = [vp, ul, vp, vp, vp, vp, vp]
+        L.fd_ed25519_gpu_verify_dev_timed.argtypes = [vp, ul, vp, ul, vp, vp, vp, vp]
         L.fd_ed25519_gpu_verify_dev_timed.restype = ip
         L.fd_ed25519_gpu_kernel_cnt.argtypes = []
         L.fd_ed25519_gpu_kernel_cnt.restype = ip
@@ -91,6 +91,12 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_poll.restype = ip
         L.fd_ed25519_gpu_depth.argtypes = [vp]
         L.fd_ed25519_gpu_depth.restype = ip
+        L.fd_ed25519_gpu_set_timeout.argtypes = [vp, ctypes.c_long]
+        L.fd_ed25519_gpu_set_timeout.restype = ip
+        L.fd_ed25519_gpu_timeout.argtypes = [vp]
+        L.fd_ed25519_gpu_timeout.restype = ctypes.c_long
+        L.fd_ed25519_gpu_wait_selftest.argtypes = [ctypes.c_long, ctypes.c_long]
+        L.fd_ed25519_gpu_wait_selftest.restype = ip
         L.fd_ed25519_gpu_device.argtypes = [vp]
         L.fd_ed25519_gpu_device.restype = ip
         L.fd_ed25519_gpu_last_error.argtypes = []
@@ -133,6 +139,8 @@ def lib() -> ctypes.CDLL:
         L.fd_vt_tcache_insert.restype = ip
         L.fd_vt_tcache_delete.argtypes = [vp]
         L.fd_vt_tcache_delete.restype = None
+        L.fd_ed25519_gpu_debug_k.argtypes = [vp, ul, vp, ul, vp, vp, vp]
+        L.fd_ed25519_gpu_debug_k.restype = ip
         L.fd_ed25519_gpu_sha512_packed.argtypes = [vp, ul, vp, ul, vp, vp, ip]
         L.fd_ed25519_gpu_sha512_packed.restype = ip
         L.fd_ed25519_gpu_default.argtypes = []
@@ -200,6 +208,7 @@ class Engine:
         self.device = device
         self.max_sigs = max_sigs
         self.max_blob = max_blob
+        self._pending = {}
 
     def close(self):
         if self._h:
@@ -222,34 +231,70 @@ class Engine:
             raise EngineError(f"verify_packed: {strerror(err)}: {last_error()}")
         return out
 
-    def verify_dev(self, n: int, d_blob: int, d_desc: int, d_out: int, stream: int = 0) -> None:
-        """Device-resident batch (raw device pointers, e.g. torch tensor .data_ptr())."""
-        err = lib().fd_ed25519_gpu_verify_dev(self._h, n, d_blob, d_desc, d_out, stream or None)
+    def verify_dev(self, n: int, d_blob: int, blob_sz: int, d_desc: int, d_out: int, stream: int = 0) -> None:
+        """Device-resident batch (raw device pointers, e.g. torch tensor .data_ptr());
+        blob_sz = payload bytes at d_blob (descriptors are bounds-checked against it)."""
+        err = lib().fd_ed25519_gpu_verify_dev(self._h, n, d_blob, blob_sz, d_desc, d_out, stream or None)
         if err:
             raise EngineError(f"verify_dev: {strerror(err)}: {last_error()}")
 
     KERNELS = ("fd_k_prep", "fd_k_decomp", "fd_k_dsm_setup", "fd_k_dsm_pool", "fd_k_dsm_final")
 
-    def verify_dev_timed(self, n: int, d_blob: int, d_desc: int, d_out: int, stream: int = 0) -> np.ndarray:
+    def verify_dev_timed(self, n: int, d_blob: int, blob_sz: int, d_desc: int, d_out: int, stream: int = 0) -> np.ndarray:
         """verify_dev with per-kernel HIP-event durations (ms), in KERNELS order."""
         ms = np.zeros(lib().fd_ed25519_gpu_kernel_cnt(), np.float32)
-        err = lib().fd_ed25519_gpu_verify_dev_timed(self._h, n, d_blob, d_desc, d_out, stream or None, _p(ms))
+        err = lib().fd_ed25519_gpu_verify_dev_timed(self._h, n, d_blob, blob_sz, d_desc, d_out, stream or None, _p(ms))
         if err:
             raise EngineError(f"verify_dev_timed: {strerror(err)}: {last_error()}")
         return ms
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
+        """Queue a batch on the pinned ring; returns its ticket."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
         t = ctypes.c_ulong(0)
         err = lib().fd_ed25519_gpu_submit(self._h, len(desc), _p(blob), blob.nbytes, _p(desc), ctypes.byref(t))
         if err:
             raise EngineError(f"submit: {strerror(err)}: {last_error()}")
+        self._pending[t.value] = len(desc)
         return t.value
 
     def poll(self, ticket: int, out: np.ndarray, block: bool = True) -> bool:
+        """Collect a ticket's codes into out (int32, contiguous, >= the batch's
+        signature count); False while the batch is in flight."""
+        n = self._pending.get(ticket)
+        if n is None:
+            raise EngineError(f"poll: unknown ticket {ticket}")
+        if not isinstance(out, np.ndarray) or out.dtype != np.int32 or not out.flags.c_contiguous or out.size < n:
+            raise EngineError(f"poll: out must be a contiguous int32 array of >= {n} entries")
         r = lib().fd_ed25519_gpu_poll(self._h, ticket, _p(out), 1 if block else 0)
         if r < 0:
             raise EngineError(f"poll: {strerror(r)}: {last_error()}")
+        if r == 1:
+            del self._pending[ticket]
         return r == 1
+
+    @property
+    def timeout_ns(self) -> int:
+        """bound on one blocking wait (ns; < 0 unbounded)"""
+        return lib().fd_ed25519_gpu_timeout(self._h)
+
+    @timeout_ns.setter
+    def timeout_ns(self, ns: int) -> None:
+        if lib().fd_ed25519_gpu_set_timeout(self._h, int(ns)):
+            raise EngineError("set_timeout")
+
+    def debug_k(self, blob: np.ndarray, desc: np.ndarray):
+        """Diagnostics: (k[n,32], status[n]) from fd_k_prep -- k = SHA-512(R||A||M)
+        mod L for signatures whose S check is pending (status 1), else zeros."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        k = np.zeros((len(desc), 32), np.uint8)
+        st = np.zeros(len(desc), np.int32)
+        err = lib().fd_ed25519_gpu_debug_k(self._h, len(desc), _p(blob), blob.nbytes, _p(desc), _p(k), _p(st))
+        if err:
+            raise EngineError(f"debug_k: {strerror(err)}: {last_error()}")
+        return k, st
 
     def sha512(self, msgs, is384: bool = False) -> list:
         """SHA-512 (SHA-384) digests of byte strings on the device."""

@@ -298,8 +298,24 @@ CASES = [
 def adversarial(n, msg_sz=128, seed=0, invalid_frac=0.1, nthreads=8):
     """C3: (1-invalid_frac) valid signatures, the rest split evenly over the
     invalid cases above.  Returns a Batch whose .label holds the case index."""
-    base = simple(n, msg_sz, seed, nthreads)
-    rng = np.random.default_rng(seed + 7919)
+    return corrupt(simple(n, msg_sz, seed, nthreads), seed + 7919, invalid_frac)
+
+
+def adversarial_txns(n, seed=0, invalid_frac=0.1, nthreads=8, **kw):
+    """C3 at C2 shape: Solana-MTU txns (solana_txns; msg 1167 / 1103 B) with
+    invalid_frac of the signatures corrupted over all the cases above.  In a
+    txn the signer keys are part of the signed message, so a case that
+    rewrites a key also changes its co-signers' message (the reference
+    decides every code; the label names only what was done)."""
+    return corrupt(solana_txns(n, seed=seed, nthreads=nthreads, **kw), seed + 7919, invalid_frac)
+
+
+def corrupt(base, seed, invalid_frac=0.1, cases=None):
+    """Corrupt invalid_frac of base's signatures in place, split evenly over
+    CASES[1:] (or the named subset `cases`); .label receives the case index."""
+    n = len(base)
+    pick = [CASES.index(c) for c in cases] if cases else list(range(1, len(CASES)))
+    rng = np.random.default_rng(seed)
     blob = base.blob
     desc = base.desc
     label = np.zeros(n, np.int8)
@@ -309,7 +325,7 @@ def adversarial(n, msg_sz=128, seed=0, invalid_frac=0.1, nthreads=8):
     offc = off_curve_encodings(64, rng)
     torsion = [pt for pt in torsion_points() if pt != (0, 1)]
     for j, i in enumerate(idx):
-        case = 1 + (j % (len(CASES) - 1))
+        case = pick[j % len(pick)]
         label[i] = case
         name = CASES[case]
         so, po, mo, ms = (int(desc[i][f]) for f in ("sig_off", "pub_off", "msg_off", "msg_sz"))

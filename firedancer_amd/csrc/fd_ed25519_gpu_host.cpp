@@ -30,26 +30,77 @@
 #endif
 #define FD_BLOB_PAD  64UL
 
-/* offset of the descriptors in a slot's staging buffer for a blob of
-   blob_sz bytes */
-/* blocking polls spin this long before sleeping */
-#define FD_POLL_SPIN_NS 20000000L
+static thread_local char fd_gpu_err[256];
 
-/* Wait for a slot's completion event: spin on it for up to
-   FD_POLL_SPIN_NS (as a tile busy-polls its rings; hipEventSynchronize's
-   wake-up adds tens of microseconds to a ~0.7 ms batch round trip), then
-   sleep in hipEventSynchronize. */
-static hipError_t fd_event_wait( hipEvent_t ev ) {
-  hipError_t e = hipEventQuery( ev );
-  if( e != hipErrorNotReady ) return e;
-  struct timespec t0, t1;
-  clock_gettime( CLOCK_MONOTONIC, &t0 );
+static int fd_gpu_fail( char const * what, hipError_t e ) {
+  snprintf( fd_gpu_err, sizeof(fd_gpu_err), "%s: %s", what, hipGetErrorString( e ) );
+  return FD_ED25519_ERR_GPU;
+}
+static void fd_gpu_fail_q( char const * what, hipError_t e ) { (void)fd_gpu_fail( what, e ); }
+
+/* blocking polls spin this long before they start sleeping between queries */
+#define FD_POLL_SPIN_NS 20000000L
+/* default bound on one blocking wait (fd_ed25519_gpu_set_timeout): a
+   4096-signature batch takes ~0.8 ms and a 1M-signature launch ~17 ms, so
+   10 s only fires on a wedged queue (the reference's accelerator poll is
+   bounded the same way, src/wiredancer/c/wd_f1.h:25 WD_TRY_LIMIT) */
+#define FD_WAIT_TIMEOUT_NS_DEFAULT 10000000000L
+
+static inline long fd_now_ns( void ) {
+  struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t );
+  return (long)t.tv_sec * 1000000000L + (long)t.tv_nsec;
+}
+
+/* Bounded wait on a completion query: spin (as a tile busy-polls its
+   rings; a sleeping wake-up adds tens of microseconds to a ~0.8 ms batch
+   round trip) for up to spin_ns, then query every ~50 us until timeout_ns
+   (< 0: no bound).  query returns 1 ready, 0 not yet, < 0 failed.  Returns
+   1 ready, 0 timed out, < 0 the query's failure. */
+static int fd_wait_query( int (*query)( void * ), void * ctx, long spin_ns, long timeout_ns ) {
+  int r = query( ctx );
+  if( r ) return r;
+  long t0 = fd_now_ns();
   for(;;) {
-    __builtin_ia32_pause();
-    if( (e = hipEventQuery( ev )) != hipErrorNotReady ) return e;
-    clock_gettime( CLOCK_MONOTONIC, &t1 );
-    if( (t1.tv_sec - t0.tv_sec) * 1000000000L + (t1.tv_nsec - t0.tv_nsec) > FD_POLL_SPIN_NS ) return hipEventSynchronize( ev );
+    long dt = fd_now_ns() - t0;
+    if( timeout_ns >= 0 && dt > timeout_ns ) return 0;
+    if( dt <= spin_ns ) __builtin_ia32_pause();
+    else { struct timespec ts = { 0, 50000L }; nanosleep( &ts, NULL ); }
+    if( (r = query( ctx )) ) return r;
   }
+}
+
+static int fd_event_query( void * ev ) {
+  hipError_t e = hipEventQuery( (hipEvent_t)ev );
+  if( e == hipSuccess ) return 1;
+  if( e == hipErrorNotReady ) return 0;
+  fd_gpu_fail_q( "hipEventQuery", e );
+  return -1;
+}
+
+/* wait for a slot's completion event: 0 done, FD_ED25519_ERR_GPU on a
+   runtime failure or after timeout_ns (the batch may still complete; the
+   caller may poll again) */
+static int fd_event_wait( hipEvent_t ev, long timeout_ns ) {
+  int r = fd_wait_query( fd_event_query, (void *)ev, FD_POLL_SPIN_NS, timeout_ns );
+  if( r == 1 ) return 0;
+  if( r == 0 ) {
+    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "wait: batch not complete after %ld ms", timeout_ns / 1000000L );
+    return FD_ED25519_ERR_GPU;
+  }
+  return FD_ED25519_ERR_GPU;
+}
+
+/* Self-test of the bounded wait without a device (tests/test_abi.py): a
+   fake completion that becomes ready ready_after_ns after the call (< 0:
+   never, a stuck batch).  Returns 1 ready, 0 timed out. */
+struct fd_fake_ticket { long ready_at; };
+static int fd_fake_query( void * ctx ) {
+  fd_fake_ticket * f = (fd_fake_ticket *)ctx;
+  return f->ready_at >= 0 && fd_now_ns() >= f->ready_at;
+}
+extern "C" int fd_ed25519_gpu_wait_selftest( long timeout_ns, long ready_after_ns ) {
+  fd_fake_ticket f = { ready_after_ns < 0 ? -1L : fd_now_ns() + ready_after_ns };
+  return fd_wait_query( fd_fake_query, &f, 1000000L, timeout_ns );
 }
 
 static inline unsigned long fd_desc_off( unsigned long blob_sz ) { return (blob_sz + FD_BLOB_PAD + 15UL) & ~15UL; }
@@ -71,6 +122,7 @@ struct fd_ed25519_gpu_slot {
   unsigned long           n;
   unsigned long           ticket;   /* 0 = free */
   int                     staged;   /* pinned buffers lent out by fd_ed25519_gpu_stage */
+  int                     orphan;   /* a synchronous call timed out on it: reclaimed once its event completes */
   uint8_t *               h_dig;    /* pinned digests (SHA-512 batch), allocated on first use */
 };
 
@@ -84,17 +136,18 @@ struct fd_ed25519_gpu {
   unsigned long pool_min; /* batches >= this take the pooled DSM */
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
+  long          timeout_ns; /* bound on one blocking wait (< 0: none) */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
+  /* device-resident path (verify_dev / _timed): its own HBM working set,
+     so it never shares scratch with a ring batch; dev_done orders
+     successive device-resident launches on whatever streams they come */
+  fd_ed25519_gpu_work_t dev_work;
+  void *        d_dev_work_base;
+  hipEvent_t    dev_done;
+  std::mutex    dev_lock;
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
 };
-
-static thread_local char fd_gpu_err[256];
-
-static int fd_gpu_fail( char const * what, hipError_t e ) {
-  snprintf( fd_gpu_err, sizeof(fd_gpu_err), "%s: %s", what, hipGetErrorString( e ) );
-  return FD_ED25519_ERR_GPU;
-}
 
 #define HIPCHK(call) do { hipError_t e_ = (call); if( e_ != hipSuccess ) { fd_gpu_fail( #call, e_ ); goto fail; } } while(0)
 
@@ -145,6 +198,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
+  g->timeout_ns = FD_WAIT_TIMEOUT_NS_DEFAULT;
   /* a slot's pinned and device blob buffers also hold the batch's
      descriptors, 16-aligned after the padded blob, so a batch is ONE H2D
      copy (a second small copy costs ~17 us of a ~0.75 ms 4096-signature
@@ -194,6 +248,10 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
       }
     }
   }
+  HIPCHK( hipMalloc( &g->d_dev_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
+  fd_work_carve( &g->dev_work, g->d_dev_work_base, max_sigs );
+  HIPCHK( hipEventCreateWithFlags( &g->dev_done, hipEventDisableTiming ) );
+  HIPCHK( hipEventRecord( g->dev_done, g->slot[0].stream ) );
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
   return g;
 fail:
@@ -201,13 +259,32 @@ fail:
   return NULL;
 }
 
+static int fd_stream_query( void * st ) {
+  hipError_t e = hipStreamQuery( (hipStream_t)st );
+  return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -1;
+}
+
 extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   if( !g ) return;
   hipSetDevice( g->device );
+  /* drain every stream, each wait bounded: if the device is wedged the
+     engine's memory is leaked rather than freed under a running kernel */
+  long to = g->timeout_ns;
+  for( int s=0; s<g->depth; s++ ) {
+    hipStream_t sts[2] = { g->slot[s].stream, g->slot[s].mstream };
+    for( int k=0; k<2; k++ )
+      if( sts[k] && fd_wait_query( fd_stream_query, (void *)sts[k], FD_POLL_SPIN_NS, to ) != 1 ) {
+        snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
+        return;
+      }
+  }
+  if( g->dev_done && fd_wait_query( fd_event_query, (void *)g->dev_done, FD_POLL_SPIN_NS, to ) != 1 ) {
+    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
+    return;
+  }
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
-    if( sl->stream ) hipStreamSynchronize( sl->stream );
-    if( sl->mstream ) { hipStreamSynchronize( sl->mstream ); hipStreamDestroy( sl->mstream ); }
+    if( sl->mstream ) hipStreamDestroy( sl->mstream );
     if( sl->h_blob ) hipHostFree( sl->h_blob );
     if( sl->h_desc ) hipHostFree( sl->h_desc );
     if( sl->h_out  ) hipHostFree( sl->h_out );
@@ -219,11 +296,21 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     if( sl->stream ) hipStreamDestroy( sl->stream );
     if( sl->done   ) hipEventDestroy( sl->done );
   }
+  if( g->dev_done ) hipEventDestroy( g->dev_done );
+  if( g->d_dev_work_base ) hipFree( g->d_dev_work_base );
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->kev[k] ) hipEventDestroy( g->kev[k] );
   delete g;
 }
 
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
+
+extern "C" int fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long timeout_ns ) {
+  if( !g ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  g->timeout_ns = timeout_ns;
+  return 0;
+}
+extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? g->timeout_ns : 0L; }
 
 extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
   if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE && mode != FD_ED25519_GPU_MODE_STRICT) ) return FD_ED25519_ERR_ARG;
@@ -266,70 +353,74 @@ extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob 
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) g->slot[s].staged = 0;
 }
 
-/* a free slot: the staged one owning `blob` if any, else any unstaged one */
+/* a free slot: the staged one owning `blob` if any, else any unstaged one
+   (slots orphaned by a timed-out synchronous call come back once done) */
 static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * blob ) {
+  for( int s=0; s<g->depth; s++ ) {
+    fd_ed25519_gpu_slot * sl = &g->slot[s];
+    if( sl->orphan && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->ticket = 0; }
+  }
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && g->slot[s].h_blob == blob ) return &g->slot[s];
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) return &g->slot[s];
   return NULL;
 }
 extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? g->device : -1; }
 
-/* Bounds check one descriptor against the blob (the reference does no
-   argument checking, fd_ed25519.h:89; malformed txns are dropped
-   upstream by fd_txn_parse -- the batch API reports them itself). */
-static inline int fd_desc_ok( fd_ed25519_gpu_desc_t const * d, unsigned long blob_sz ) {
-  return (unsigned long)d->sig_off + 64UL <= blob_sz
-      && (unsigned long)d->pub_off + 32UL <= blob_sz
-      && (unsigned long)d->msg_off + (unsigned long)d->msg_sz <= blob_sz;
-}
-
-extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob,
-                                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream ) {
-  if( !g || n > g->max_sigs ) return FD_ED25519_ERR_ARG;
-  if( !n ) return 0;
+/* The device-resident path.  Descriptors are bounds-checked on the device
+   against blob_sz (fd_k_prep reports FD_ED25519_ERR_ARG, nothing reads
+   outside the blob).  Launches serialise on the engine's device-resident
+   working set: each waits (on the device) for the previous one, whatever
+   stream either came on. */
+static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
+                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, hipEvent_t const * ev ) {
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->mode, g->pool_min, g->quad_max );
+  if( (e = hipStreamWaitEvent( st, g->dev_done, 0 )) != hipSuccess ) return fd_gpu_fail( "hipStreamWaitEvent", e );
+  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work, (int32_t *)d_out, st, ev,
+                                   g->mode, g->pool_min, g->quad_max );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
+  if( (e = hipEventRecord( g->dev_done, st )) != hipSuccess ) return fd_gpu_fail( "hipEventRecord", e );
   return 0;
 }
 
-extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob,
+extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
+                                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream ) {
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->dev_lock );
+  return fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, NULL );
+}
+
+extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
                                                 fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream,
                                                 float * kernel_ms ) {
-  if( !g || n > g->max_sigs || !kernel_ms ) return FD_ED25519_ERR_ARG;
-  hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
-  hipError_t e = hipSetDevice( g->device );
-  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, d_desc, &g->slot[0].work, (int32_t *)d_out, st, g->kev, g->mode, g->pool_min, g->quad_max );
-  if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
-  if( (e = hipEventSynchronize( g->kev[FD_ED25519_GPU_KERNEL_CNT] )) != hipSuccess ) return fd_gpu_fail( "sync", e );
-  for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
-    kernel_ms[k] = 0.f;
-    if( n && (e = hipEventElapsedTime( &kernel_ms[k], g->kev[k], g->kev[k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
-  }
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || !kernel_ms || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
+  for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) kernel_ms[k] = 0.f;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->dev_lock );
+  int err = fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, g->kev );
+  if( err ) return err;
+  if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], g->timeout_ns )) ) return err;
+  hipError_t e;
+  for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ )
+    if( (e = hipEventElapsedTime( &kernel_ms[k], g->kev[k], g->kev[k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
   return 0;
 }
 
 extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_CNT; }
 
 /* Stage a batch into a slot's pinned buffers and enqueue copy-in,
-   kernels, copy-out on the slot's stream. */
-static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
-                            unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
+   kernels, copy-out on the slot's stream.  Descriptors are copied as
+   given: the device checks each against blob_sz and reports an
+   out-of-bounds one as FD_ED25519_ERR_ARG (fd_k_prep). */
+static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
+                             unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, hipStream_t * used ) {
   if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
   unsigned long doff = fd_desc_off( blob_sz );
   memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
-  /* descriptors land after the padded blob (one copy); out-of-bounds ones
-     are replaced by a harmless in-bounds one and reported as
-     FD_ED25519_ERR_ARG after the run */
-  fd_ed25519_gpu_desc_t * hd = (fd_ed25519_gpu_desc_t *)(sl->h_blob + doff);
-  for( unsigned long i=0; i<n; i++ ) {
-    fd_ed25519_gpu_desc_t d = desc[i];
-    if( !fd_desc_ok( &d, blob_sz ) ) { d.sig_off = d.pub_off = d.msg_off = 0; d.msg_sz = 0; }
-    hd[i] = d;
-  }
+  /* descriptors land after the padded blob (one copy) */
+  memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   hipError_t e;
   /* the slot's CU group only while another ring batch is in flight (a
      lone batch runs faster spread over the whole device: depth-1 p50
@@ -339,10 +430,11 @@ static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsi
     for( int s=0; s<g->depth; s++ )
       if( &g->slot[s] != sl && g->slot[s].ticket && hipEventQuery( g->slot[s].done ) == hipErrorNotReady ) others = 1;
   hipStream_t st = others ? sl->mstream : sl->stream;
+  *used = st;
   if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
@@ -351,9 +443,19 @@ static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsi
   return 0;
 }
 
-static void fd_slot_collect( fd_ed25519_gpu_slot * sl, unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, int * out ) {
-  for( unsigned long i=0; i<sl->n; i++ ) out[i] = sl->h_out[i];
-  if( desc ) for( unsigned long i=0; i<sl->n; i++ ) if( !fd_desc_ok( &desc[i], blob_sz ) ) out[i] = FD_ED25519_ERR_ARG;
+/* On failure, whatever was already queued on the slot's stream (the H2D
+   copy from its pinned buffer, kernels on its scratch) is drained before
+   the slot can be picked again. */
+static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
+                            unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
+  hipStream_t st = NULL;
+  int err = fd_slot_enqueue_( g, sl, n, blob, blob_sz, desc, &st );
+  if( err && st ) (void)hipStreamSynchronize( st );
+  return err;
+}
+
+static void fd_slot_collect( fd_ed25519_gpu_slot * sl, int * out ) {
+  memcpy( out, sl->h_out, sl->n * sizeof(int) );
 }
 
 extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
@@ -368,8 +470,12 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   if( !sl ) return FD_ED25519_ERR_ARG;   /* every slot in flight or lent out */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
-  if( (e = fd_event_wait( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
-  fd_slot_collect( sl, blob_sz, desc, out );
+  if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) {
+    sl->ticket = g->next_ticket++;   /* still in flight: the slot is not reused until it drains */
+    sl->orphan = 1;
+    return err;
+  }
+  fd_slot_collect( sl, out );
   return 0;
 }
 
@@ -384,7 +490,6 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
   sl->staged = 0;
-  /* keep what collect needs for the bounds report */
   sl->ticket = g->next_ticket++;
   *ticket = sl->ticket;
   return 0;
@@ -398,13 +503,67 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
-  hipError_t e = block ? fd_event_wait( sl->done ) : hipEventQuery( sl->done );
-  if( e == hipErrorNotReady ) return 0;
-  if( e != hipSuccess ) return fd_gpu_fail( "poll", e );
+  if( block ) {
+    int err = fd_event_wait( sl->done, g->timeout_ns );
+    if( err ) return err;               /* timed out or failed; the ticket stays valid */
+  } else {
+    hipError_t e = hipEventQuery( sl->done );
+    if( e == hipErrorNotReady ) return 0;
+    if( e != hipSuccess ) return fd_gpu_fail( "poll", e );
+  }
   std::lock_guard<std::mutex> guard( g->lock );
-  if( out ) fd_slot_collect( sl, ~0UL, NULL, out );
+  if( out ) fd_slot_collect( sl, out );
   sl->ticket = 0;
   return 1;
+}
+
+/* Diagnostics: k = SHA-512(R||A||M) mod L of each signature, computed by
+   fd_k_prep on the device (the SURVEY.md section 7 minimum-slice check:
+   compared with the reference's fd_sha512_* + fd_ed25519_sc_reduce,
+   fd_ed25519_user.c:411-414).  k_out receives n x 32 bytes; signatures
+   the S check settles (and malformed descriptors) get 32 zero bytes and
+   status_out[i] != 1 (the reference computes no k for them either).
+   Synchronous; host buffers. */
+extern "C" int fd_ed25519_gpu_debug_k( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                       fd_ed25519_gpu_desc_t const * desc, uint8_t * k_out, int * status_out ) {
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!desc || !k_out || !status_out)) || (blob_sz && !blob) )
+    return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<std::mutex> dguard( g->dev_lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
+  if( !sl ) return FD_ED25519_ERR_ARG;
+  hipStream_t st = sl->stream;
+  unsigned long doff = fd_desc_off( blob_sz );
+  memcpy( sl->h_blob, blob, blob_sz );
+  memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
+  memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  uint64_t * d_k = (uint64_t *)g->dev_work.tab;   /* 1536 B of table scratch per signature >= 32 */
+  uint64_t * h_k = (uint64_t *)malloc( 32UL * n );
+  int32_t * h_st = (int32_t *)malloc( 4UL * n );
+  int err = 0;
+  if( !h_k || !h_st ) { err = FD_ED25519_ERR_GPU; goto done; }
+  if( (e = hipStreamWaitEvent( st, g->dev_done, 0 )) != hipSuccess
+   || (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess
+   || (e = hipMemsetAsync( d_k, 0, 32UL * n, st )) != hipSuccess
+   || (e = fd_ed25519_gpu_launch_prep_k( n, sl->d_blob, blob_sz, (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff), &g->dev_work, d_k, st )) != hipSuccess
+   || (e = hipMemcpyAsync( h_k, d_k, 32UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
+   || (e = hipMemcpyAsync( h_st, g->dev_work.status, 4UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
+   || (e = hipEventRecord( sl->done, st )) != hipSuccess
+   || (e = hipEventRecord( g->dev_done, st )) != hipSuccess ) { err = fd_gpu_fail( "debug_k", e ); (void)hipStreamSynchronize( st ); goto done; }
+  if( (err = fd_event_wait( g->dev_done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; goto done; }
+  for( unsigned long i=0; i<n; i++ ) {
+    status_out[i] = h_st[i];
+    for( int j=0; j<4; j++ ) {
+      uint64_t w = h_st[i] == 1 ? h_k[(unsigned long)j*n + i] : 0UL;
+      for( int b=0; b<8; b++ ) k_out[32UL*i + 8UL*(unsigned long)j + (unsigned long)b] = (uint8_t)(w >> (8*b));
+    }
+  }
+done:
+  free( h_k ); free( h_st );
+  return err;
 }
 
 /* SHA-512 / SHA-384 of n messages blob[msg_off..+msg_sz) (sig_off and
@@ -435,7 +594,9 @@ extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long
     return fd_gpu_fail( "launch sha512", e );
   if( (e = hipMemcpyAsync( sl->h_dig, d_dig, n * 64UL, hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "D2H digests", e );
-  if( (e = hipStreamSynchronize( sl->stream )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+  if( (e = hipEventRecord( sl->done, sl->stream )) != hipSuccess ) return fd_gpu_fail( "event", e );
+  int err = fd_event_wait( sl->done, g->timeout_ns );
+  if( err ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
   unsigned long hsz = is384 ? 48UL : 64UL;
   for( unsigned long i=0; i<n; i++ ) memcpy( (uint8_t *)hash_out + i*hsz, sl->h_dig + i*64UL, hsz );
   sl->staged = 0;
@@ -470,6 +631,10 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
                              uint8_t const * const * pubp, uint8_t const (*puba)[32], int * out ) {
   fd_ed25519_gpu_t * g = fd_default_engine();
   if( !g ) return FD_ED25519_ERR_GPU;
+  /* every message must fit one engine blob: checked before any chunk runs,
+     so ERR_ARG writes nothing (fd_ed25519_gpu.h) */
+  if( shared_msg ) { if( shared_sz > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG; }
+  else for( unsigned long k=0; k<n; k++ ) if( msg_sz[k] > 0x7fffffffUL || msg_sz[k] > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
@@ -480,14 +645,10 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
     /* fill one chunk */
     unsigned long used = 0, cnt = 0;
     unsigned long shared_off = 0;
-    if( shared_msg ) {
-      if( shared_sz + 96UL > g->max_blob ) return FD_ED25519_ERR_ARG;
-      memcpy( sl->h_blob, shared_msg, shared_sz ); used = shared_sz;
-    }
+    if( shared_msg ) { memcpy( sl->h_blob, shared_msg, shared_sz ); used = shared_sz; }
     while( i + cnt < n && cnt < g->max_sigs ) {
       unsigned long k = i + cnt;
       unsigned long msz = shared_msg ? 0UL : msg_sz[k];
-      if( msz > 0x7fffffffUL ) return FD_ED25519_ERR_ARG;
       if( used + 96UL + msz > g->max_blob ) break;
       fd_ed25519_gpu_desc_t * d = &sl->h_desc[cnt];
       d->sig_off = (uint32_t)used; memcpy( sl->h_blob + used, sigp ? sigp[k] : siga[k], 64 ); used += 64;
@@ -500,10 +661,9 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
       }
       cnt++;
     }
-    if( !cnt ) return FD_ED25519_ERR_ARG;   /* single message larger than the engine's blob */
     int err = fd_slot_enqueue( g, sl, cnt, sl->h_blob, used, sl->h_desc );
     if( err ) return err;
-    if( (e = fd_event_wait( sl->done )) != hipSuccess ) return fd_gpu_fail( "sync", e );
+    if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
     for( unsigned long k=0; k<cnt; k++ ) out[i+k] = sl->h_out[k];
     i += cnt;
   }

@@ -106,11 +106,16 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 #include "fd_ed25519_gpu_wnaf.h"
 
 static __device__ __forceinline__ void
-fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+              fd_ed25519_gpu_desc_t const * __restrict__ desc,
               int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-              uint8_t * sha_stage ) {
+              uint8_t * sha_stage, uint64_t * __restrict__ kout ) {
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
+  /* a descriptor outside the blob is reported, never dereferenced (the
+     reference does no argument checking, fd_ed25519.h:89, so the engine
+     owns this code; it takes precedence over every other result) */
+  if( !fd_desc_in( d, blob_sz ) ) { status[i] = FD_ED25519_ERR_ARG; op_start[i] = FD_OPS_MAX; return; }
   uint8_t const * R = blob + d.sig_off;
   uint8_t const * S = R + 32;
   uint8_t const * A = blob + d.pub_off;
@@ -139,6 +144,10 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25
   fd_sha512_ram( dig, R, A, M, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
   uint64_t k[4];
   fd_sc_reduce( k, dig );
+  if( kout ) {   /* diagnostics (fd_ed25519_gpu_debug_k): k = SHA-512(R||A||M) mod L, [4][n] */
+#pragma unroll
+    for( int j=0; j<4; j++ ) kout[(uint64_t)j*n + i] = k[j];
+  }
 
   /* recode k and S into the op stream (fd_ed25519_gpu_wnaf.h) */
   uint32_t kw[8];
@@ -148,10 +157,11 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4)
-fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict ) {
+fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+           int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
+           uint64_t * __restrict__ kout ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
-  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, ops, op_start, strict, sha_stage );
+  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, kout );
 }
 
 /* ------------------------------------------------------------------ */
@@ -219,8 +229,8 @@ FD_DEV int fd_limbs_eq( fe const & a, fe const & b ) {
 /* status may be NULL (fd_k_front: prep runs concurrently, so nothing is
    skipped; the DSM's code precedence puts a failed S check first anyway) */
 static __device__ __forceinline__ void
-fd_decomp_body( uint64_t j, uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
-                int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
+fd_decomp_body( uint64_t j, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+                fd_ed25519_gpu_desc_t const * __restrict__ desc, int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
                 int portable, int strict ) {
   /* portable mode (ref/fd_ed25519_ge.c:242-288 via fd_ed25519_user.c:
      400-403 with 2POINT 0): only A is decompressed (the grid covers
@@ -230,6 +240,9 @@ fd_decomp_body( uint64_t j, uint64_t n, uint8_t const * __restrict__ blob, fd_ed
   uint64_t i = j < n ? j : j - n;
   if( status && status[i] != FD_ST_PENDING ) { pstat[j] = FD_PT_OK; return; }
   fd_ed25519_gpu_desc_t d = desc[i];
+  /* malformed descriptor: prep reports ERR_ARG (fd_k_front runs the two
+     side by side, so decomp checks for itself instead of reading status) */
+  if( !fd_desc_in( d, blob_sz ) ) { pstat[j] = FD_PT_OK; return; }
   uint8_t const * s = blob + (j < n ? d.pub_off : d.sig_off);
   uint32_t w[8]; fd_ld32( w, s );
 
@@ -298,10 +311,10 @@ fd_decomp_body( uint64_t j, uint64_t n, uint8_t const * __restrict__ blob, fd_ed
 }
 
 extern "C" __global__ void __launch_bounds__(256)
-fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
              int32_t const * __restrict__ status, int32_t * __restrict__ pstat, int32_t * __restrict__ pts,
              int portable, int strict ) {
-  fd_decomp_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, pstat, pts, portable, strict );
+  fd_decomp_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, pstat, pts, portable, strict );
 }
 
 /* Latency front end (batches on the quad schedule): prep and decomp have
@@ -318,14 +331,14 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_
 #define FD_FRONT_WAVES 1
 #endif
 extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
-fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
   if( blockIdx.x < nb_prep )
-    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, desc, status, ops, op_start, strict, sha_stage );
+    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, NULL );
   else
-    fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, desc, NULL, pstat, pts, portable, strict );
+    fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
 }
 
 /* ------------------------------------------------------------------ */
@@ -538,7 +551,9 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
 
   if( portable ) {
     /* canonical encoding of R compared with the signature's r bytes
-       (fd_ed25519_user.c:428-431, ref/fd_ed25519_ge.c:367-375) */
+       (fd_ed25519_user.c:428-431, ref/fd_ed25519_ge.c:367-375); only a
+       pending signature's descriptor is known to be in bounds */
+    if( code != FD_ST_PENDING ) { if( live ) out[i] = code; return; }
     fe zi, x, y;
     fd_fe_invert( zi, Z );
     fd_fe_mul( x, X, zi );
@@ -551,7 +566,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
     uint32_t diff = 0;
 #pragma unroll
     for( int k=0; k<8; k++ ) diff |= enc[k] ^ rw[k];
-    if( code == FD_ST_PENDING ) code = diff ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS;
+    code = diff ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS;
     if( live ) out[i] = code;
     return;
   }
@@ -1201,7 +1216,7 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
   return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_tab), bi, sizeof(bi) );
 }
 
-extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                                     hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
@@ -1210,19 +1225,21 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
-  hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+  hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+  if( e != hipSuccess ) return e;
   int quad = n < pool_min && !portable && n <= quad_max;
   if( quad ) {
     /* latency path: prep and decomp in one launch (their time lands in phase 1) */
     unsigned const bt = 64u*FD_FRONT_WAVES;
     unsigned const fp = (unsigned)((n + bt - 1) / bt), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
-    hipLaunchKernelGGL( fd_k_front, dim3(fp + fd), dim3(bt), 0, stream, n, blob, desc, w->status, w->ops, w->op_start,
+    hipLaunchKernelGGL( fd_k_front, dim3(fp + fd), dim3(bt), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start,
                         w->pstat, w->pts, portable, strict, fp );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
-    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, desc, w->status, w->ops, w->op_start, strict );
+    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
+                        (uint64_t *)NULL );
     if( ev ) hipEventRecord( ev[1], stream );
-    hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, desc, w->status, w->pstat, w->pts, portable, strict );
+    hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
   }
   if( ev ) hipEventRecord( ev[2], stream );
   /* phases 3-5: DSM setup (Ai tables), DSM main loop, final compare; the
@@ -1250,8 +1267,21 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   return hipGetLastError();
 }
 
-extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+/* diagnostics: fd_k_prep alone, writing each pending signature's k as
+   [4][n] little-endian 64-bit words to kout and its prep status to w->status */
+extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz,
+                                                   fd_ed25519_gpu_desc_t const * desc, fd_ed25519_gpu_work_t const * w,
+                                                   uint64_t * kout, hipStream_t stream ) {
+  if( !n ) return hipSuccess;
+  hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+  if( e != hipSuccess ) return e;
+  hipLaunchKernelGGL( fd_k_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, blob, blob_sz, desc,
+                      w->status, w->ops, w->op_start, 0, kout );
+  return hipGetLastError();
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                               fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
                                               uint64_t pool_min, uint64_t quad_max ) {
-  return fd_ed25519_gpu_launch_timed( n, blob, desc, w, out, stream, NULL, mode, pool_min, quad_max );
+  return fd_ed25519_gpu_launch_timed( n, blob, blob_sz, desc, w, out, stream, NULL, mode, pool_min, quad_max );
 }

@@ -40,14 +40,22 @@ typedef struct fd_ed25519_gpu_work {
 extern "C" {
 #endif
 hipError_t fd_ed25519_gpu_upload_tables( void );
-hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                         fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                         hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                         fd_ed25519_gpu_work_t const * w, uint64_t * kout, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                          void * out, int is384, hipStream_t stream );
-hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
                                   uint64_t pool_min, uint64_t quad_max );
+/* descriptor bounds: R||S, the key and the message inside blob[0, blob_sz)
+   (64-bit sums, so no offset wraps) */
+static inline __host__ __device__ int fd_desc_in( fd_ed25519_gpu_desc_t const & d, uint64_t blob_sz ) {
+  return (uint64_t)d.sig_off + 64UL <= blob_sz && (uint64_t)d.pub_off + 32UL <= blob_sz
+      && (uint64_t)d.msg_off + (uint64_t)d.msg_sz <= blob_sz;
+}
 /* batches of at least this many signatures take the pooled DSM */
 #define FD_DSM_POOL_MIN_DEFAULT (262144UL)
 /* smaller batches of at most this many signatures take the quad-lane DSM */

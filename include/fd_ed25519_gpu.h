@@ -103,8 +103,9 @@ fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob )
 
 /* As fd_ed25519_gpu_new with a ring of `depth` (1..8) pinned slots /
    streams (fd_ed25519_gpu_new uses 3).  More slots keep more batches in
-   flight: a 4096-signature batch occupies 64 of the chip's 1024 SIMDs,
-   so sustained streaming wants several small batches executing at once. */
+   flight: a 4096-signature batch on the latency schedule runs as 256
+   single-wave workgroups on the chip's 1024 SIMDs, so sustained streaming
+   wants several small batches executing at once. */
 fd_ed25519_gpu_t *
 fd_ed25519_gpu_new_ex( int device, unsigned long max_sigs, unsigned long max_blob, int depth );
 
@@ -114,10 +115,18 @@ fd_ed25519_gpu_delete( fd_ed25519_gpu_t * gpu );
 unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * gpu );
 unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * gpu );
 
-/* Synchronous: host blob/desc in, host codes out.  Bounds-checks every
-   descriptor (FD_ED25519_ERR_ARG in out[i] for a malformed one).
-   Returns 0 on success (codes in out) or FD_ED25519_ERR_GPU /
-   FD_ED25519_ERR_ARG if the batch could not be run. */
+/* Descriptor bounds (every entry point): a descriptor whose signature,
+   key or message does not lie inside blob[0, blob_sz) gets
+   FD_ED25519_ERR_ARG in its out[] entry and is never dereferenced; the
+   check runs on the device (fd_k_prep), so the ring, the device-resident
+   path and the multi-device path report it identically.  The reference
+   does no argument checking (fd_ed25519.h:89); its callers pass
+   fd_txn_parse-validated offsets.
+
+   Synchronous: host blob/desc in, host codes out.  Returns 0 on success
+   (codes in out) or FD_ED25519_ERR_GPU / FD_ED25519_ERR_ARG if the batch
+   could not be run (FD_ED25519_ERR_GPU also when the batch did not
+   complete within the engine's timeout, fd_ed25519_gpu_set_timeout). */
 int
 fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t *            gpu,
                               unsigned long                 n,
@@ -126,14 +135,18 @@ fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t *            gpu,
                               fd_ed25519_gpu_desc_t const * desc,
                               int *                         out );
 
-/* Device-resident: d_blob (padded by >= 16 readable bytes), d_desc and
-   d_out are device pointers; enqueued on `stream` (a hipStream_t, NULL
-   for the engine's own stream); no host synchronisation.  Descriptors
-   must already be in bounds. */
+/* Device-resident: d_blob (blob_sz bytes, followed by >= 16 readable
+   pad bytes), d_desc and d_out are device pointers; enqueued on `stream`
+   (a hipStream_t, NULL for the engine's own stream); no host
+   synchronisation.  Descriptors are bounds-checked against blob_sz on the
+   device.  The device-resident path has its own HBM working set (it never
+   shares scratch with ring batches); successive calls are ordered on the
+   device whatever streams they are issued on. */
 int
 fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
                            unsigned long                 n,
                            void const *                  d_blob,
+                           unsigned long                 blob_sz,
                            fd_ed25519_gpu_desc_t const * d_desc,
                            int *                         d_out,
                            void *                        stream );
@@ -143,8 +156,10 @@ fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
    padded blob) and enqueues one H2D copy, the kernels and the D2H copy
    on that slot's stream; poll returns 1 and fills out when the batch has
    completed, 0 if still in flight, <0 on error (block != 0: spins on the
-   slot's event for up to 20 ms, then sleeps until it completes).  At
-   most fd_ed25519_gpu_depth() batches may be outstanding. */
+   slot's event for up to 20 ms, then sleeps between queries until it
+   completes or the engine's timeout passes: FD_ED25519_ERR_GPU, and the
+   ticket stays valid for a later poll).  At most fd_ed25519_gpu_depth()
+   batches may be outstanding. */
 int
 fd_ed25519_gpu_submit( fd_ed25519_gpu_t *            gpu,
                        unsigned long                 n,
@@ -161,6 +176,18 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
 
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
+
+/* Bound on every blocking wait of the engine, in ns (default 10 s; < 0:
+   unbounded).  A wait that exceeds it returns FD_ED25519_ERR_GPU instead
+   of hanging the caller on a wedged queue (as the reference's
+   accelerator poll is bounded, src/wiredancer/c/wd_f1.h:25). */
+int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * gpu, long timeout_ns );
+long fd_ed25519_gpu_timeout    ( fd_ed25519_gpu_t const * gpu );
+
+/* Self-test of the bounded wait, no device needed: a fake ticket that
+   completes ready_after_ns after the call (< 0: never).  Returns 1 if it
+   completed within timeout_ns, 0 if the wait timed out. */
+int  fd_ed25519_gpu_wait_selftest( long timeout_ns, long ready_after_ns );
 
 /* Reference build whose results the engine reproduces bit for bit:
      FD_ED25519_GPU_MODE_AVX (default): the AVX2 build the reference's CI
@@ -227,6 +254,7 @@ int
 fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t *            gpu,
                                  unsigned long                 n,
                                  void const *                  d_blob,
+                                 unsigned long                 blob_sz,
                                  fd_ed25519_gpu_desc_t const * d_desc,
                                  int *                         d_out,
                                  void *                        stream,

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/config_digests.json: the reference's own
+per-signature codes (oracle/_ref/libfdref.so, the AVX2 fd_ed25519_verify
+built in place from /root/reference by oracle/Makefile) over the
+deterministic, seeded BASELINE-size corpora of SURVEY.md section 8d,
+recorded as a SHA-256 digest of the int8 code vector plus a histogram.
+
+The corpora are regenerated on the GPU box from their seeds
+(firedancer_amd.corpus: numpy's seeded generator + the product's
+deterministic host signer), so tests/test_gpu_configs.py can pin the
+engine's codes to the reference even where the reference build is not
+shipped; where it is, the tests also compare code by code.
+
+  c1     1,048,576 x (128-byte msg), all valid                    (C1)
+  c3c2   1,048,576 signatures of Solana-MTU txns (msg 1167/1103 B), 10 %
+         corrupted over all 18 invalid cases                      (C3 at C2 shape)
+  c4     one 256-byte / 442-byte message, n = 1..16 and 4096 signers,
+         25 % of the signatures corrupted (signature/key cases only)  (C4)
+
+Runs only in the build container (needs the reference build)."""
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("FD_ED25519_NO_TORCH", "1")
+
+from firedancer_amd import corpus  # noqa: E402
+
+C1 = {"n": 1 << 20, "msg_sz": 128, "seed": 4101}
+C3C2 = {"n": 1 << 20, "seed": 4102, "invalid_frac": 0.1}
+C4_SIZES = (256, 442)
+C4_NS = list(range(1, 17)) + [4096]
+C4_CASES = ["flip_R", "flip_S", "flip_pub", "S_eq_L", "S_eq_L1", "S_top_big", "S_q1_early_accept",
+            "noncanon_A", "noncanon_R", "small_A", "small_R", "small_both", "offcurve_A", "offcurve_R",
+            "mixed_order_A", "negzero_A", "negzero_R"]
+
+
+def digest(codes):
+    return hashlib.sha256(np.ascontiguousarray(codes, np.int8).tobytes()).hexdigest()
+
+
+def hist(codes):
+    u, c = np.unique(codes, return_counts=True)
+    return {str(int(a)): int(b) for a, b in zip(u, c)}
+
+
+def c1_batch(nthreads=8):
+    return corpus.simple(C1["n"], C1["msg_sz"], seed=C1["seed"], nthreads=nthreads)
+
+
+def c3c2_batch(nthreads=8):
+    return corpus.adversarial_txns(C3C2["n"], seed=C3C2["seed"], invalid_frac=C3C2["invalid_frac"], nthreads=nthreads)
+
+
+def c4_batch(msg_sz, n, nthreads=8):
+    """(batch, shared msg, sig[n,64], pub[n,32]) for one C4 case"""
+    b, msg, _, _ = corpus.single_msg(n, msg_sz, seed=5000 + 100 * n + msg_sz, nthreads=nthreads)
+    corpus.corrupt(b, seed=6000 + 100 * n + msg_sz, invalid_frac=0.25, cases=C4_CASES)
+    sig, pub, _, _, _ = b.flat()
+    return b, bytes(msg), sig, pub
+
+
+def ref_codes(L, b, threads=8):
+    sig, pub, data, off, sz = b.flat()
+    out = np.zeros(len(b), np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    L.ref_verify_batch(ctypes.c_ulong(len(b)), P(sig), P(pub), P(data), P(off), P(sz), P(out), threads)
+    return out
+
+
+def main():
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libfdref.so"))
+    res = {"generator": "tests/golden/make_config_digests.py", "checker": "oracle/_ref/libfdref.so (reference AVX2 build)"}
+    b = c1_batch()
+    e = ref_codes(L, b)
+    res["c1"] = dict(C1, digest=digest(e), hist=hist(e))
+    del b
+    b = c3c2_batch()
+    e = ref_codes(L, b)
+    res["c3c2"] = dict(C3C2, digest=digest(e), hist=hist(e), label_hist=hist(b.label))
+    del b
+    c4 = {}
+    for sz in C4_SIZES:
+        for n in C4_NS:
+            b, _, _, _ = c4_batch(sz, n)
+            e = ref_codes(L, b)
+            c4[f"{sz}/{n}"] = {"codes": e.tolist()} if n <= 16 else {"digest": digest(e), "hist": hist(e)}
+    res["c4"] = {"sizes": list(C4_SIZES), "ns": C4_NS, "cases": C4_CASES, "expected": c4}
+    json.dump(res, open(os.path.join(HERE, "config_digests.json"), "w"), indent=1)
+    print(json.dumps({k: v.get("hist") for k, v in res.items() if isinstance(v, dict) and "hist" in v}))
+
+
+if __name__ == "__main__":
+    main()

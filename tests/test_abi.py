@@ -76,3 +76,19 @@ def test_corpus_shapes():
     assert set(np.unique(b.desc["msg_sz"]).tolist()) <= {1167, 1103}
     a = corpus.adversarial(400, 128, seed=1)
     assert (a.label > 0).sum() == 40
+
+
+def test_bounded_wait_selftest():
+    """fd_event_wait's bounded poll (fd_ed25519_gpu_set_timeout) on a fake
+    ticket, no device: a stuck ticket times out in about the timeout, a
+    late one completes (the reference bounds its accelerator poll the
+    same way, src/wiredancer/c/wd_f1.h:25)"""
+    import time
+    L = fa.lib()
+    t0 = time.perf_counter()
+    assert L.fd_ed25519_gpu_wait_selftest(30_000_000, -1) == 0          # never ready: 30 ms timeout
+    dt = time.perf_counter() - t0
+    assert 0.025 < dt < 1.0, dt
+    assert L.fd_ed25519_gpu_wait_selftest(2_000_000_000, 40_000_000) == 1  # ready after 40 ms (past the spin)
+    assert L.fd_ed25519_gpu_wait_selftest(2_000_000_000, 0) == 1
+    assert L.fd_ed25519_gpu_wait_selftest(1_000_000, 500_000_000) == 0   # late: timed out first

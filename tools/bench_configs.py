@@ -35,15 +35,16 @@ def ref_codes(ref, b, threads):
 
 def dev_throughput(eng, b, reps, torch):
     dev = torch.device("cuda", 0)
+    blob_sz = len(b.blob)
     d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
     d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
     d_out = torch.zeros(len(b), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
-    eng.verify_dev(len(b), d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), st)
+    eng.verify_dev(len(b), d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), st)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        eng.verify_dev(len(b), d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), st)
+        eng.verify_dev(len(b), d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return len(b) * reps / dt, d_out.cpu().numpy()

@@ -32,21 +32,22 @@ def main():
         d = src.desc[:n].copy()
         hi = int(max((d["msg_off"] + d["msg_sz"]).max(), d["sig_off"].max() + 64))
         blob = np.ascontiguousarray(src.blob[:hi])
+        blob_sz = len(blob)
         d_blob = torch.from_numpy(np.concatenate([blob, np.zeros(64, np.uint8)])).to(dev)
         d_desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         d_out = torch.zeros(n, dtype=torch.int32, device=dev)
         for _ in range(5):
-            eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
+            eng.verify_dev_timed(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
         reps = 30
         ks = np.zeros((reps, len(fa.Engine.KERNELS)))
         for r in range(reps):
-            ks[r] = eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
+            ks[r] = eng.verify_dev_timed(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
         ok = bool((d_out == 0).all().item())
         # device-resident wall per launch (no events)
         torch.cuda.synchronize()
         t = time.perf_counter()
         for _ in range(reps):
-            eng.verify_dev(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
+            eng.verify_dev(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
         torch.cuda.synchronize()
         dev_ms = (time.perf_counter() - t) / reps * 1e3
         # depth-1 host round trip

@@ -20,16 +20,17 @@ def main():
     batch.desc = batch.desc[:n]
     eng = fa.Engine(0, max_sigs=n, max_blob=max(len(batch.blob), 1 << 24))
     dev = torch.device("cuda", 0)
+    blob_sz = len(batch.blob)
     d_blob = torch.from_numpy(np.concatenate([batch.blob, np.zeros(64, np.uint8)])).to(dev)
     d_desc = torch.from_numpy(batch.desc.view(np.uint8).copy()).to(dev)
     d_out = torch.zeros(n, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(3):
-        eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
+        eng.verify_dev_timed(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
     ks = np.zeros(len(fa.Engine.KERNELS))
     reps = 10
     for _ in range(reps):
-        ks += eng.verify_dev_timed(n, d_blob.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), s)
+        ks += eng.verify_dev_timed(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
     ks /= reps
     ok = bool((d_out == 0).all().item())
     print(os.environ.get("FD_ED25519_LIB", "default"), " ".join(f"{k[5:]}={v:.4f}" for k, v in zip(fa.Engine.KERNELS, ks)),
