@@ -17,8 +17,10 @@ RCCL only carries the timing barrier and the max-over-ranks.
 Extra measurements on rank 0 at N=1:
   roofline     per-kernel HIP-event durations over the timed launches,
                algorithmic int32 ops / duration
-  latency      submit -> results-on-host of single 4096-signature batches
-               through the pinned-ring pipeline (PCIe inclusive), p50/p99
+  latency      C2 at its own granularity: 4096-signature batches streamed
+               through the per-GPU feeder and the engine's pinned ring
+               (PCIe both ways included): verifies/s and push -> codes-on-
+               host p50/p99 at ring depth 6 (4 CU groups), 4 and 1
   cpu_baseline the reference's own fd_ed25519_verify (oracle/_ref build,
                'reference') or the CPU restatement ('port') on a bounded
                sample of the same corpus, all host threads of this rank
@@ -60,12 +62,16 @@ N_DBL, N_ADD = 251.5, 84.9
 # DSM, split as the engine runs it (avx/fd_ed25519_ge.c:423-523,
 #   fd_ed25519_user.c:419-427):
 #   fd_k_dsm_setup: Ai table, 92 mul + 3 sq + 1 sq2 + 8 x 30 mix ops;
-#   fd_k_dsm_pool:  each doubling SQN(1,1,1,2) + one 4-lane conversion MUL,
-#                   each addition one 4-lane MUL + conversion MUL, lane mixes
-#                   DBL_MIX+X+Y 50, SUBADD_12+SUB_MIX 70 int32 ops;
+#   fd_k_dsm_pool:  each doubling SQN(1,1,1,2) + the p1p1->p2 conversion's 3
+#                   MULs (X, Y, Z: the reference's 4-lane MUL leaves its 4th
+#                   lane idle, avx/fd_ed25519_ge.c:521-522; the kernel issues
+#                   3, fd_pool_dbl), each addition the 4-lane p3 conversion
+#                   MUL + the 4-lane op MUL = 8 MULs, lane mixes DBL_MIX+X+Y
+#                   50, SUBADD_12+SUB_MIX 70 int32 ops (3,140
+#                   field ops per verify counts the conversion as 3);
 #   fd_k_dsm_final: p2 conversion 3 mul + compare 2 mul.
 SLOTS_DSM_SETUP = 92 * SLOT_MUL + 3 * SLOT_SQ + SLOT_SQ2 + 240
-SLOTS_DSM_LOOP = ((4 * N_DBL + 8 * N_ADD) * SLOT_MUL + 3 * N_DBL * SLOT_SQ + N_DBL * SLOT_SQ2
+SLOTS_DSM_LOOP = ((3 * N_DBL + 8 * N_ADD) * SLOT_MUL + 3 * N_DBL * SLOT_SQ + N_DBL * SLOT_SQ2
                   + 50 * N_DBL + 70 * N_ADD)
 SLOTS_DSM_FINAL = 5 * SLOT_MUL
 SLOTS_DSM = SLOTS_DSM_SETUP + SLOTS_DSM_LOOP + SLOTS_DSM_FINAL
@@ -93,36 +99,72 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
+    ap.add_argument("--ring-depth", type=int, default=6, help="ring slots of the C2 streaming leg")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
+def usable_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by
+    the cgroup CPU quota (a GPU box grants a job a share of the host: its
+    os.cpu_count() is the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _time_checker(L, fn, sub, threads):
+    import ctypes
+    sig, pub, data, off, sz = sub.flat()
+    out = np.zeros(len(sub), np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    t0 = time.perf_counter()
+    getattr(L, fn)(ctypes.c_uint64(len(sub)), P(sig), P(pub), P(data), P(off), P(sz), P(out), threads)
+    dt = time.perf_counter() - t0
+    assert (out == 0).all(), f"CPU baseline ({fn}) rejected valid signatures"
+    return dt
+
+
 def cpu_baseline(batch, nsig, threads):
-    """Time the reference build (preferred) or the CPU restatement over a
-    bounded sample of the same corpus."""
+    """The reference's own fd_ed25519_verify (oracle/_ref/libfdref.so, the
+    AVX2 build compiled from /root/reference; 'reference') timed on a
+    bounded sample of the same corpus on every core this job may use, plus
+    the SURVEY.md 8d calibration ratio: the CPU restatement
+    (oracle/liboracle.so) / the reference on the same sample, same box.
+    Falls back to the restatement ('port') only if the reference build
+    was not shipped, and says so."""
     import ctypes
     ref = os.path.join(ROOT, "oracle", "_ref", "libfdref.so")
     port = os.path.join(ROOT, "oracle", "liboracle.so")
-    if os.path.exists(ref):
-        L, kind, fn = ctypes.CDLL(ref), "reference", "ref_verify_batch"
-    elif os.path.exists(port):
-        L, kind, fn = ctypes.CDLL(port), "port", "oracle_verify_batch"
-    else:
-        return None
     sub = batch.tile(int(math.ceil(nsig / len(batch))))
     sub.desc = sub.desc[:nsig]
-    sig, pub, data, off, sz = sub.flat()
-    out = np.zeros(nsig, np.int32)
-    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    t0 = time.perf_counter()
-    getattr(L, fn)(ctypes.c_uint64(nsig), P(sig), P(pub), P(data), P(off), P(sz), P(out), threads)
-    dt = time.perf_counter() - t0
-    assert (out == 0).all(), "CPU baseline rejected valid signatures"
-    return {"value": nsig / dt, "unit": "verifies/s", "cores": threads, "kind": kind,
-            "sample": f"{nsig} signatures of the same C2 corpus (1232-byte txns, msg 1167/1103 B), "
-                      f"{threads} host threads, {dt:.2f} s wall ({dt * threads:.1f} thread-s)",
-            "cpu": _cpu_model()}
+    res = {"unit": "verifies/s", "cores": threads, "cpu": _cpu_model(), "host_cpus_visible": os.cpu_count()}
+    if os.path.exists(ref):
+        dt = _time_checker(ctypes.CDLL(ref), "ref_verify_batch", sub, threads)
+        res.update(value=nsig / dt, kind="reference")
+    elif os.path.exists(port):
+        dt = _time_checker(ctypes.CDLL(port), "oracle_verify_batch", sub, threads)
+        res.update(value=nsig / dt, kind="port", note="reference build not shipped: restatement timed")
+    else:
+        return None
+    res["per_core"] = res["value"] / threads
+    res["sample"] = (f"{nsig} signatures of the same C2 corpus (1232-byte txns, msg 1167/1103 B), "
+                     f"{threads} host threads (all this job may use), {dt:.2f} s wall ({dt * threads:.1f} thread-s)")
+    if res["kind"] == "reference" and os.path.exists(port):
+        cal = batch.tile(1)
+        cal.desc = cal.desc[:min(len(cal), max(threads * 2048, 16384))]
+        t_ref = _time_checker(ctypes.CDLL(ref), "ref_verify_batch", cal, threads)
+        t_port = _time_checker(ctypes.CDLL(port), "oracle_verify_batch", cal, threads)
+        res["calibration"] = {"restatement_over_reference": t_ref / t_port, "sample_sigs": len(cal),
+                              "note": "throughput ratio of the CPU restatement to the reference build, same "
+                                      "sample and threads on this box (SURVEY.md 8d)"}
+    return res
 
 
 def _cpu_model():
@@ -276,11 +318,15 @@ def main():
                             "VALU-bound, traffic is a secondary check",
         }
         if not a.no_latency:
-            res["latency"] = latency(eng, base, a.latency_batches)
+            # C2 at its own granularity: 4096-signature batches through the
+            # per-GPU feeder and pinned ring, PCIe both ways included
+            res["latency"] = ring_stream(fa, base, local, a.latency_batches, a.ring_depth)
+            res["latency"]["lower_latency_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), 4)
             # one batch in flight at a time: the per-batch floor
-            res["latency"]["depth1"] = latency(eng, base, max(a.latency_batches // 5, 20), depth=1)
+            res["latency"]["depth1"] = ring_stream(fa, base, local, max(a.latency_batches // 5, 20), 1)
+            res["ring_4096_verifies_per_s"] = res["latency"]["pcie_inclusive_verifies_per_s"]
         if not a.no_cpu:
-            res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, min(16, os.cpu_count() or 8))
+            res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, usable_cores())
         res["corpus_gen_s"] = gen_s
 
     if rank == 0:
@@ -289,44 +335,62 @@ def main():
         dist.destroy_process_group()
 
 
-def latency(eng, base, nb, depth=None):
-    """Single 4096-signature batches, host pinned ring -> GPU -> host,
-    depth-deep pipeline kept full (default: every ring slot); submit ->
-    completion per batch."""
-    nb = max(nb, 20)
-    depth = min(depth or eng.depth, eng.depth)
-    starts = np.random.default_rng(7).integers(0, len(base) - BATCH_SIGS, nb)
-    # each batch: its own compacted blob (the txn payload bytes it references)
-    jobs = []
-    for s in starts[: min(nb, 64)]:
-        d = base.desc[s:s + BATCH_SIGS].copy()
-        lo = int(min(d["sig_off"].min(), d["pub_off"].min(), d["msg_off"].min()))
-        hi = int(max((d["msg_off"] + d["msg_sz"]).max(), d["sig_off"].max() + 64))
-        for f in ("sig_off", "pub_off", "msg_off"):
-            d[f] -= lo
-        jobs.append((np.ascontiguousarray(base.blob[lo:hi]), d))
-    out = np.zeros(BATCH_SIGS, np.int32)
-    lat = []
-    inflight = []
-    t_all = time.perf_counter()
-    for i in range(nb):
-        blob, d = jobs[i % len(jobs)]
-        if len(inflight) == depth:
-            t, ts = inflight.pop(0)
-            eng.poll(t, out, block=True)
-            lat.append(time.perf_counter() - ts)
-        ts = time.perf_counter()
-        inflight.append((eng.submit(blob, d), ts))
-    for t, ts in inflight:
-        eng.poll(t, out, block=True)
-        lat.append(time.perf_counter() - ts)
-    wall = time.perf_counter() - t_all
-    lat = np.array(lat[depth:]) * 1e3  # drop the ramp
-    return {"batch_sigs": BATCH_SIGS, "batches": nb, "pipeline_depth": depth,
-            "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
-            "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
-            "dsm_schedule": "quad" if 0 < BATCH_SIGS <= eng.dsm_quad_max and BATCH_SIGS < eng.dsm_pool_min else "uniform",
-            "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall}
+def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7):
+    """C2 at its own granularity: nb 4096-signature batches streamed through
+    one engine's pinned ring by its per-GPU feeder thread
+    (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
+    ways included.  The corpus blob is registered with the engine (as a
+    tile registers its input dcache), so a batch is DMA'd from where it
+    lies with no staging memcpy.  `window` batches are outstanding at any
+    time (default: the ring depth, so no batch waits in the feeder's
+    queue); latency = push -> codes on the host."""
+    eng = fa.Engine(device, max_sigs=BATCH_SIGS, max_blob=8 << 20, depth=depth)
+    try:
+        if groups:
+            eng.cu_groups = groups
+        if register:
+            eng.register(base.blob)
+        feeder = fa.Feeder(eng)
+        starts = np.random.default_rng(seed).integers(0, len(base) - BATCH_SIGS, 64)
+        descs = [np.ascontiguousarray(base.desc[s:s + BATCH_SIGS]) for s in starts]
+        W = window or depth
+        jobs = [fa.Job() for _ in range(W)]
+        outs = [np.full(BATCH_SIGS, 99, np.int32) for _ in range(W)]
+        lat, qlat, ok = [], [], True
+
+        def done(k):
+            nonlocal ok
+            feeder.wait(jobs[k])
+            j = jobs[k]
+            lat.append((j.t_done_ns - j.t_push_ns) * 1e-6)
+            qlat.append((j.t_done_ns - j.t_submit_ns) * 1e-6)
+            ok = ok and bool((outs[k] == 0).all())
+
+        t0 = time.perf_counter()
+        for i in range(nb):
+            k = i % W
+            if i >= W:
+                done(k)
+            feeder.push(base.blob, descs[i % len(descs)], outs[k], jobs[k])
+        for i in range(nb, nb + W):
+            if i - W < nb and i >= W:
+                done(i % W)
+        wall = time.perf_counter() - t0
+        numa = feeder.numa_node
+        feeder.close()
+        lat = np.array(lat[W:]) if len(lat) > 2 * W else np.array(lat)
+        qlat = np.array(qlat[W:]) if len(qlat) > 2 * W else np.array(qlat)
+        return {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
+                "cu_groups": eng.cu_groups, "registered_source": bool(register),
+                "feeder_numa_node": numa,
+                "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
+                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+                "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
+                "submit_to_done_p50_ms": float(np.percentile(qlat, 50)),
+                "submit_to_done_p99_ms": float(np.percentile(qlat, 99)),
+                "all_accepted": ok}
+    finally:
+        eng.close()
 
 
 if __name__ == "__main__":

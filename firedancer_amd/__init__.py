@@ -169,6 +169,28 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_multi_verify_packed.restype = ip
         L.fd_ed25519_codes_to_bitmap.argtypes = [ul, vp, vp]
         L.fd_ed25519_codes_to_bitmap.restype = None
+        L.fd_ed25519_gpu_set_cu_groups.argtypes = [vp, ip]
+        L.fd_ed25519_gpu_set_cu_groups.restype = ip
+        L.fd_ed25519_gpu_cu_groups.argtypes = [vp]
+        L.fd_ed25519_gpu_cu_groups.restype = ip
+        L.fd_ed25519_gpu_register.argtypes = [vp, vp, ul]
+        L.fd_ed25519_gpu_register.restype = ip
+        L.fd_ed25519_gpu_unregister.argtypes = [vp, vp]
+        L.fd_ed25519_gpu_unregister.restype = ip
+        L.fd_ed25519_gpu_feeder_new.argtypes = [vp, ip]
+        L.fd_ed25519_gpu_feeder_new.restype = vp
+        L.fd_ed25519_gpu_feeder_delete.argtypes = [vp]
+        L.fd_ed25519_gpu_feeder_delete.restype = None
+        L.fd_ed25519_gpu_feeder_numa_node.argtypes = [vp]
+        L.fd_ed25519_gpu_feeder_numa_node.restype = ip
+        L.fd_ed25519_gpu_feeder_push.argtypes = [vp, vp]
+        L.fd_ed25519_gpu_feeder_push.restype = ip
+        L.fd_ed25519_gpu_job_wait.argtypes = [vp, ctypes.c_long]
+        L.fd_ed25519_gpu_job_wait.restype = ip
+        L.fd_ed25519_gpu_multi_new_ex.argtypes = [vp, ip, ul, ul, ip]
+        L.fd_ed25519_gpu_multi_new_ex.restype = vp
+        L.fd_ed25519_gpu_multi_feeder.argtypes = [vp, ip]
+        L.fd_ed25519_gpu_multi_feeder.restype = vp
         L.fd_sha512_gpu_batch_new.argtypes = [vp, ip]
         L.fd_sha512_gpu_batch_new.restype = vp
         L.fd_sha512_gpu_batch_delete.argtypes = [vp]
@@ -209,6 +231,7 @@ class Engine:
         self.max_sigs = max_sigs
         self.max_blob = max_blob
         self._pending = {}
+        self._registered = []
 
     def close(self):
         if self._h:
@@ -350,14 +373,91 @@ class Engine:
     def depth(self) -> int:
         return lib().fd_ed25519_gpu_depth(self._h)
 
+    @property
+    def cu_groups(self) -> int:
+        """CU groups the ring's small batches are spread over (1: none)"""
+        return lib().fd_ed25519_gpu_cu_groups(self._h)
+
+    @cu_groups.setter
+    def cu_groups(self, g: int) -> None:
+        if lib().fd_ed25519_gpu_set_cu_groups(self._h, int(g)):
+            raise EngineError(f"set_cu_groups({g}): ring busy or bad count")
+
+    def register(self, host: np.ndarray) -> None:
+        """Let the ring DMA batches straight from this (contiguous) host array."""
+        if not host.flags.c_contiguous:
+            raise EngineError("register: array must be contiguous")
+        if lib().fd_ed25519_gpu_register(self._h, _p(host), host.nbytes):
+            raise EngineError(f"register: {last_error()}")
+        self._registered.append(host)
+
+    def unregister(self, host: np.ndarray) -> None:
+        if lib().fd_ed25519_gpu_unregister(self._h, _p(host)):
+            raise EngineError(f"unregister: {last_error()}")
+        self._registered = [a for a in self._registered if a is not host]
+
+
+class Job(ctypes.Structure):
+    """fd_ed25519_gpu_job_t"""
+    _fields_ = [("n", ctypes.c_ulong), ("blob", ctypes.c_void_p), ("blob_sz", ctypes.c_ulong),
+                ("desc", ctypes.c_void_p), ("out", ctypes.c_void_p), ("state", ctypes.c_int),
+                ("t_push_ns", ctypes.c_ulong), ("t_submit_ns", ctypes.c_ulong), ("t_done_ns", ctypes.c_ulong)]
+
+
+class Feeder:
+    """The per-GPU feeder thread (fd_ed25519_gpu_feeder_t) over an Engine's ring."""
+
+    def __init__(self, engine: Engine, pin_numa: bool = True):
+        self.engine = engine
+        self._h = lib().fd_ed25519_gpu_feeder_new(engine._h, 1 if pin_numa else 0)
+        if not self._h:
+            raise EngineError("fd_ed25519_gpu_feeder_new failed")
+        self._keep = {}
+
+    @property
+    def numa_node(self) -> int:
+        return lib().fd_ed25519_gpu_feeder_numa_node(self._h)
+
+    def push(self, blob: np.ndarray, desc: np.ndarray, out: np.ndarray, job: Job = None) -> Job:
+        """Queue a batch; the arrays must stay alive and unchanged until the job completes."""
+        if blob.dtype != np.uint8 or not blob.flags.c_contiguous or desc.dtype != DESC_DTYPE or not desc.flags.c_contiguous:
+            raise EngineError("push: contiguous uint8 blob and DESC_DTYPE desc required")
+        if out.dtype != np.int32 or not out.flags.c_contiguous or out.size < len(desc):
+            raise EngineError("push: out must be a contiguous int32 array of >= len(desc) entries")
+        j = job if job is not None else Job()
+        j.n, j.blob, j.blob_sz, j.desc, j.out = len(desc), blob.ctypes.data, blob.nbytes, desc.ctypes.data, out.ctypes.data
+        self._keep[ctypes.addressof(j)] = (blob, desc, out)
+        err = lib().fd_ed25519_gpu_feeder_push(self._h, ctypes.byref(j))
+        if err:
+            raise EngineError(f"feeder push: {strerror(err)}")
+        return j
+
+    def wait(self, job: Job, timeout_ns: int = -1) -> None:
+        err = lib().fd_ed25519_gpu_job_wait(ctypes.byref(job), timeout_ns)
+        self._keep.pop(ctypes.addressof(job), None)
+        if err:
+            raise EngineError(f"job: {strerror(err)}: {last_error()}")
+
+    def close(self):
+        if self._h:
+            lib().fd_ed25519_gpu_feeder_delete(self._h)
+            self._h = None
+            self._keep.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
 
 class MultiEngine:
     """Engines on several devices (repeats allowed) behind one host:
     fd_ed25519_gpu_multi_t."""
 
-    def __init__(self, devices, max_sigs: int = 1 << 16, max_blob: int = 1 << 26):
+    def __init__(self, devices, max_sigs: int = 1 << 16, max_blob: int = 1 << 26, depth: int = 3):
         d = np.ascontiguousarray(devices, np.int32)
-        self._h = lib().fd_ed25519_gpu_multi_new(_p(d), len(d), max_sigs, max_blob)
+        self._h = lib().fd_ed25519_gpu_multi_new_ex(_p(d), len(d), max_sigs, max_blob, depth)
         if not self._h:
             raise EngineError(f"fd_ed25519_gpu_multi_new({list(devices)}) failed: {last_error()}")
 

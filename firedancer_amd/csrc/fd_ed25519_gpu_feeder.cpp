@@ -1,0 +1,253 @@
+/* fd_ed25519_gpu_feeder.cpp -- the per-GPU host feeder of SURVEY.md
+   section 8e: one host thread per engine, pinned to the CPUs of the
+   GPU's NUMA node, that keeps the engine's pinned ring full.
+
+   Jobs (a batch of descriptors into a caller blob) are queued by any
+   thread; the feeder thread
+     - copies the byte span the job's descriptors reference into a free
+       ring slot (the one host copy; none when the span lies in a region
+       registered with fd_ed25519_gpu_register: the slot DMAs it in place)
+       with the descriptors rebased to the span,
+     - submits it (H2D, the kernels, D2H on the slot's stream),
+     - and, while later jobs are staged and submitted, collects completed
+       batches oldest first, writing the codes to the job's out[] and
+       releasing its state word.
+   So with a ring of depth D, up to D batches are in flight and batch
+   k+1's staging copy overlaps batch k's transfers and kernels.
+
+   The reference has no GPU feeder; its accelerator precedent streams
+   requests to the FPGA from the parser tile and polls with a bounded
+   retry (src/wiredancer/c/wd_f1.c:327-407, WD_TRY_LIMIT in wd_f1.h:25).
+   The same bound applies here through the engine's timeout. */
+
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include "fd_ed25519_gpu.h"
+
+#define FD_EXPORT extern "C" __attribute__((visibility("default")))
+
+static inline unsigned long fd_feeder_now( void ) {
+  struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t );
+  return (unsigned long)t.tv_sec * 1000000000UL + (unsigned long)t.tv_nsec;
+}
+
+struct fd_feeder_inflight {
+  fd_ed25519_gpu_job_t * job;
+  unsigned long          ticket;
+};
+
+struct fd_ed25519_gpu_feeder {
+  fd_ed25519_gpu_t *                   gpu;
+  std::thread                          th;
+  std::mutex                           lock;
+  std::condition_variable              cv;
+  std::deque<fd_ed25519_gpu_job_t *>   queue;
+  std::deque<fd_feeder_inflight>       inflight;
+  std::vector<unsigned long>           zombies;     /* tickets of batches given up on (timed out): drained later */
+  std::vector<fd_ed25519_gpu_desc_t>   rebased;
+  std::atomic<int>                     halt;
+  int                                  numa_node;   /* -1: not pinned */
+  int                                  cpu_cnt;     /* CPUs in the pinned set */
+  unsigned long                        max_sigs, max_blob;
+};
+
+/* The CPUs of device's NUMA node that this process may use (the PCI
+   function's numa_node in sysfs, that node's cpulist, intersected with
+   the current affinity mask).  Returns the node or -1. */
+static int fd_feeder_numa_cpus( int device, cpu_set_t * set ) {
+  char bdf[64];
+  if( hipDeviceGetPCIBusId( bdf, (int)sizeof(bdf), device ) != hipSuccess ) return -1;
+  for( char * c = bdf; *c; c++ ) if( *c >= 'A' && *c <= 'F' ) *c = (char)(*c - 'A' + 'a');
+  char path[160];
+  snprintf( path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bdf );
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1;
+  int node = -1;
+  if( fscanf( f, "%d", &node ) != 1 ) node = -1;
+  fclose( f );
+  if( node < 0 ) return -1;
+  snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
+  f = fopen( path, "r" );
+  if( !f ) return -1;
+  cpu_set_t node_set; CPU_ZERO( &node_set );
+  int a, b; char sep;
+  while( fscanf( f, "%d", &a ) == 1 ) {
+    b = a;
+    if( fscanf( f, "%c", &sep ) == 1 && sep == '-' ) { if( fscanf( f, "%d", &b ) != 1 ) b = a; if( fscanf( f, "%c", &sep ) != 1 ) sep = 0; }
+    for( int c=a; c<=b && c<CPU_SETSIZE; c++ ) CPU_SET( c, &node_set );
+  }
+  fclose( f );
+  cpu_set_t cur; CPU_ZERO( &cur );
+  if( sched_getaffinity( 0, sizeof(cur), &cur ) ) return -1;
+  CPU_AND( set, &node_set, &cur );
+  return CPU_COUNT( set ) ? node : -1;
+}
+
+static void fd_job_finish( fd_ed25519_gpu_job_t * j, int state ) {
+  j->t_done_ns = fd_feeder_now();
+  __atomic_store_n( &j->state, state, __ATOMIC_RELEASE );
+}
+
+/* stage + submit one job; 1 submitted, 0 ring full (retry later), < 0 the job failed (finished) */
+static int fd_feeder_submit( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
+  fd_ed25519_gpu_desc_t const * d = j->desc;
+  unsigned long n = j->n, b0 = ~0UL, b1 = 0UL;
+  for( unsigned long i=0; i<n; i++ ) {
+    unsigned long lo = d[i].sig_off, hi = (unsigned long)d[i].sig_off + 64UL;
+    if( (unsigned long)d[i].pub_off + 32UL > j->blob_sz || hi > j->blob_sz
+     || (unsigned long)d[i].msg_off + (unsigned long)d[i].msg_sz > j->blob_sz ) continue;   /* ERR_ARG on the device */
+    if( d[i].pub_off < lo ) lo = d[i].pub_off;
+    if( d[i].msg_off < lo ) lo = d[i].msg_off;
+    if( (unsigned long)d[i].pub_off + 32UL > hi ) hi = (unsigned long)d[i].pub_off + 32UL;
+    if( (unsigned long)d[i].msg_off + d[i].msg_sz > hi ) hi = (unsigned long)d[i].msg_off + d[i].msg_sz;
+    if( lo < b0 ) b0 = lo;
+    if( hi > b1 ) b1 = hi;
+  }
+  if( b0 == ~0UL ) { b0 = 0UL; b1 = 0UL; }
+  if( b1 - b0 > f->max_blob ) { fd_job_finish( j, FD_ED25519_ERR_ARG ); return -1; }
+  fd_ed25519_gpu_desc_t * rd = f->rebased.data();
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_ed25519_gpu_desc_t x = d[i];
+    if( (unsigned long)x.sig_off + 64UL <= j->blob_sz && (unsigned long)x.pub_off + 32UL <= j->blob_sz
+     && (unsigned long)x.msg_off + (unsigned long)x.msg_sz <= j->blob_sz ) {
+      x.sig_off -= (uint32_t)b0; x.pub_off -= (uint32_t)b0; x.msg_off -= (uint32_t)b0;
+    } else { x.sig_off = x.pub_off = x.msg_off = 0xffffffffu; x.msg_sz = 0; }   /* stays out of bounds */
+    rd[i] = x;
+  }
+  unsigned long ticket = 0;
+  int err = fd_ed25519_gpu_submit( f->gpu, n, (uint8_t const *)j->blob + b0, b1 - b0, rd, &ticket );
+  if( err == FD_ED25519_ERR_ARG ) return 0;                       /* every slot in flight */
+  if( err ) { fd_job_finish( j, err ); return -1; }
+  j->t_submit_ns = fd_feeder_now();
+  f->inflight.push_back( fd_feeder_inflight{ j, ticket } );
+  return 1;
+}
+
+/* collect the oldest in-flight batch: 1 collected (or failed), 0 not
+   yet.  A batch not done within the engine's timeout fails its job with
+   FD_ED25519_ERR_GPU; its slot is reclaimed if it ever completes. */
+static int fd_feeder_collect( fd_ed25519_gpu_feeder_t * f ) {
+  for( size_t k=0; k<f->zombies.size(); ) {
+    if( fd_ed25519_gpu_poll( f->gpu, f->zombies[k], NULL, 0 ) != 0 ) { f->zombies[k] = f->zombies.back(); f->zombies.pop_back(); }
+    else k++;
+  }
+  if( f->inflight.empty() ) return 0;
+  fd_feeder_inflight x = f->inflight.front();
+  int r = fd_ed25519_gpu_poll( f->gpu, x.ticket, x.job->out, 0 );
+  if( r == 0 ) {
+    long to = fd_ed25519_gpu_timeout( f->gpu );
+    if( to < 0 || fd_feeder_now() - x.job->t_submit_ns <= (unsigned long)to ) return 0;
+    f->zombies.push_back( x.ticket );
+    r = FD_ED25519_ERR_GPU;
+  }
+  f->inflight.pop_front();
+  fd_job_finish( x.job, r == 1 ? 1 : r );
+  return 1;
+}
+
+static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
+  if( f->numa_node >= 0 ) {
+    cpu_set_t set; CPU_ZERO( &set );
+    if( fd_feeder_numa_cpus( fd_ed25519_gpu_device( f->gpu ), &set ) >= 0 ) pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+  }
+  (void)hipSetDevice( fd_ed25519_gpu_device( f->gpu ) );
+  int depth = fd_ed25519_gpu_depth( f->gpu );
+  fd_ed25519_gpu_job_t * pending = NULL;          /* popped, waiting for a free slot */
+  for(;;) {
+    int progress = 0;
+    /* keep the ring full */
+    while( (int)f->inflight.size() < depth ) {
+      if( !pending ) {
+        std::lock_guard<std::mutex> g( f->lock );
+        if( f->queue.empty() ) break;
+        pending = f->queue.front(); f->queue.pop_front();
+      }
+      int r = fd_feeder_submit( f, pending );
+      if( r == 0 ) break;
+      pending = NULL; progress = 1;
+    }
+    /* collect what finished, oldest first, without blocking */
+    while( fd_feeder_collect( f ) ) progress = 1;
+    if( progress ) continue;
+    if( !f->inflight.empty() || !f->zombies.empty() ) {
+      /* a batch is in flight and nothing else to do: a short pause, then
+         poll again (the tile-style busy poll; one core per GPU) */
+      __builtin_ia32_pause();
+      continue;
+    }
+    std::unique_lock<std::mutex> g( f->lock );
+    if( f->queue.empty() && !pending ) {
+      if( f->halt.load() ) break;
+      f->cv.wait_for( g, std::chrono::milliseconds( 50 ) );
+    }
+  }
+}
+
+FD_EXPORT fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_feeder_new( fd_ed25519_gpu_t * gpu, int pin_numa ) {
+  if( !gpu ) return NULL;
+  fd_ed25519_gpu_feeder_t * f = new fd_ed25519_gpu_feeder_t();
+  f->gpu = gpu;
+  f->halt.store( 0 );
+  f->max_sigs = fd_ed25519_gpu_max_sigs( gpu );
+  f->max_blob = fd_ed25519_gpu_max_blob( gpu );
+  f->rebased.resize( f->max_sigs );
+  f->numa_node = -1; f->cpu_cnt = 0;
+  if( pin_numa ) {
+    cpu_set_t set; CPU_ZERO( &set );
+    f->numa_node = fd_feeder_numa_cpus( fd_ed25519_gpu_device( gpu ), &set );
+    f->cpu_cnt = f->numa_node >= 0 ? CPU_COUNT( &set ) : 0;
+  }
+  f->th = std::thread( fd_feeder_main, f );
+  return f;
+}
+
+FD_EXPORT int fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * f ) { return f ? f->numa_node : -1; }
+
+FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
+  if( !f || !j || j->n > f->max_sigs || (j->n && (!j->desc || !j->out)) || (j->blob_sz && !j->blob) ) return FD_ED25519_ERR_ARG;
+  j->t_push_ns = fd_feeder_now(); j->t_submit_ns = 0; j->t_done_ns = 0;
+  if( !j->n ) { fd_job_finish( j, 1 ); return 0; }
+  __atomic_store_n( &j->state, 0, __ATOMIC_RELEASE );
+  {
+    std::lock_guard<std::mutex> g( f->lock );
+    if( f->halt.load() ) return FD_ED25519_ERR_ARG;
+    f->queue.push_back( j );
+  }
+  f->cv.notify_one();
+  return 0;
+}
+
+FD_EXPORT int fd_ed25519_gpu_job_wait( fd_ed25519_gpu_job_t const * j, long timeout_ns ) {
+  if( !j ) return FD_ED25519_ERR_ARG;
+  unsigned long t0 = fd_feeder_now();
+  for( unsigned long it=0;; it++ ) {
+    int s = __atomic_load_n( &j->state, __ATOMIC_ACQUIRE );
+    if( s == 1 ) return 0;
+    if( s < 0 ) return s;
+    if( timeout_ns >= 0 && fd_feeder_now() - t0 > (unsigned long)timeout_ns ) return FD_ED25519_ERR_GPU;
+    if( it < 4096 ) __builtin_ia32_pause();
+    else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
+  }
+}
+
+FD_EXPORT void fd_ed25519_gpu_feeder_delete( fd_ed25519_gpu_feeder_t * f ) {
+  if( !f ) return;
+  {
+    std::lock_guard<std::mutex> g( f->lock );
+    f->halt.store( 1 );
+  }
+  f->cv.notify_one();
+  f->th.join();     /* drains: queued jobs are submitted and collected first */
+  delete f;
+}

@@ -26,8 +26,9 @@
 #define FD_GPU_DEPTH_DEFAULT 3
 #define FD_GPU_DEPTH_MAX     8
 #ifndef FD_CU_GROUPS
-#define FD_CU_GROUPS         3   /* CU groups for small ring batches (1: none) */
+#define FD_CU_GROUPS         4   /* max default CU groups for small ring batches (1: none) */
 #endif
+#define FD_REG_MAX           16  /* registered host regions per engine */
 #define FD_BLOB_PAD  64UL
 
 static thread_local char fd_gpu_err[256];
@@ -136,6 +137,9 @@ struct fd_ed25519_gpu {
   unsigned long pool_min; /* batches >= this take the pooled DSM */
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
+  int           groups;   /* CU groups the ring's slots are spread over (1: none) */
+  int           ncu;
+  struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none) */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   /* device-resident path (verify_dev / _timed): its own HBM working set,
@@ -173,6 +177,30 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
   w->pstat    = (int32_t *)p; p +=    8UL * N;
   w->op_start = (int32_t *)p; p +=    4UL * N;
   w->ops      = (uint8_t *)p; p += (unsigned long)FD_OPS_MAX * N;
+}
+
+/* (Re)create the slots' CU-masked streams: slot s runs on group s mod
+   groups (CU c in group c mod groups, so every group spans all XCDs).
+   groups <= 1 (or no CU masking on this runtime): every batch takes the
+   whole device.  Slots must be idle. */
+static void fd_cu_groups_make( fd_ed25519_gpu_t * g, int groups ) {
+  for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
+  int ncu = g->ncu, words = (ncu + 31) / 32;
+  if( groups > g->depth ) groups = g->depth;
+  if( groups < 1 || words > 32 || groups > ncu ) groups = 1;
+  g->groups = groups;
+  /* a batch fits its group at one quad-DSM wave (16 signatures) per SIMD */
+  g->mask_max = groups > 1 ? 64UL * (unsigned long)(ncu / groups) : 0UL;
+  for( int s=0; groups > 1 && s<g->depth; s++ ) {
+    uint32_t mask[32] = { 0 };
+    for( int c=0; c<ncu; c++ ) if( c % groups == s % groups ) mask[c >> 5] |= 1u << (c & 31);
+    if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess ) {
+      (void)hipGetLastError();
+      for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
+      g->mask_max = 0UL; g->groups = 1;
+      return;
+    }
+  }
 }
 
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob ) {
@@ -231,22 +259,15 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
      SIMD) run there while other ring batches are in flight (A/B, depth 3:
      p50 0.914 -> 0.80 ms, p99 0.96 -> 0.84 ms), larger ones and lone
      batches on the whole device. */
+  g->ncu = prop.multiProcessorCount;
   {
+    /* groups scale with the ring up to 4 (64 CUs = 256 SIMDs each, one
+       4,096-signature quad-DSM batch at one wave per SIMD):
+       tools/ring_sweep.py, profiles/r02_ring_sweep.jsonl */
     int groups = g->depth < FD_CU_GROUPS ? g->depth : FD_CU_GROUPS;
-    int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
-    if( words > 32 ) groups = 1;
-    g->mask_max = groups > 1 ? 64UL * (unsigned long)(ncu / groups) : 0UL;
-    for( int s=0; groups > 1 && s<g->depth; s++ ) {
-      uint32_t mask[32] = { 0 };
-      for( int c=0; c<ncu; c++ ) if( c % groups == s % groups ) mask[c >> 5] |= 1u << (c & 31);
-      if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess ) {
-        /* no CU masking here: every batch takes the whole device */
-        (void)hipGetLastError();
-        for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
-        g->mask_max = 0UL;
-        break;
-      }
-    }
+    char const * ev = getenv( "FD_ED25519_GPU_CU_GROUPS" );    /* experiments */
+    if( ev ) groups = atoi( ev );
+    fd_cu_groups_make( g, groups );
   }
   HIPCHK( hipMalloc( &g->d_dev_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
   fd_work_carve( &g->dev_work, g->d_dev_work_base, max_sigs );
@@ -282,6 +303,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
     return;
   }
+  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p ) hipHostUnregister( (void *)g->reg[k].p );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( sl->mstream ) hipStreamDestroy( sl->mstream );
@@ -303,6 +325,54 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
 }
 
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
+
+extern "C" int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * g, int groups ) {
+  if( !g || groups < 1 || groups > FD_GPU_DEPTH_MAX ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket || g->slot[s].staged ) return FD_ED25519_ERR_ARG;   /* ring busy */
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_cu_groups_make( g, groups );
+  return 0;
+}
+extern "C" int fd_ed25519_gpu_cu_groups( fd_ed25519_gpu_t const * g ) { return g ? g->groups : 0; }
+
+/* Host regions the ring may DMA from directly (no staging copy): a batch
+   whose blob lies inside one goes H2D straight from the caller's bytes
+   (plus the descriptors from the slot's pinned buffer). */
+extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsigned long sz ) {
+  if( !g || !host || !sz ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  int k = 0;
+  while( k<FD_REG_MAX && g->reg[k].p ) k++;
+  if( k == FD_REG_MAX ) return FD_ED25519_ERR_ARG;
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  e = hipHostRegister( host, sz, hipHostRegisterPortable );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipHostRegister", e );
+  g->reg[k].p = (uint8_t const *)host; g->reg[k].sz = sz;
+  return 0;
+}
+extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
+  if( !g || !host ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p == host ) {
+    for( int s=0; s<g->depth; s++ ) {     /* no batch may still read from it */
+      fd_ed25519_gpu_slot * sl = &g->slot[s];
+      if( sl->ticket && fd_event_wait( sl->done, g->timeout_ns ) ) return FD_ED25519_ERR_GPU;
+    }
+    hipError_t e = hipHostUnregister( host );
+    g->reg[k].p = NULL; g->reg[k].sz = 0;
+    return e == hipSuccess ? 0 : fd_gpu_fail( "hipHostUnregister", e );
+  }
+  return FD_ED25519_ERR_ARG;
+}
+static int fd_registered( fd_ed25519_gpu_t const * g, void const * p, unsigned long sz ) {
+  uint8_t const * b = (uint8_t const *)p;
+  for( int k=0; k<FD_REG_MAX; k++ )
+    if( g->reg[k].p && b >= g->reg[k].p && sz <= g->reg[k].sz && (unsigned long)(b - g->reg[k].p) <= g->reg[k].sz - sz ) return 1;
+  return 0;
+}
 
 extern "C" int fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long timeout_ns ) {
   if( !g ) return FD_ED25519_ERR_ARG;
@@ -416,11 +486,18 @@ extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_
    out-of-bounds one as FD_ED25519_ERR_ARG (fd_k_prep). */
 static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
                              unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, hipStream_t * used ) {
-  if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
   unsigned long doff = fd_desc_off( blob_sz );
-  memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
-  /* descriptors land after the padded blob (one copy) */
-  memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  /* a blob in a registered region is DMA'd from where it lies (no host
+     copy; descriptors go separately from the slot's pinned desc buffer);
+     anything else is staged into the slot's pinned buffer with the
+     descriptors packed after it (one copy) */
+  int direct = sl->h_blob != blob && blob_sz && fd_registered( g, blob, blob_sz );
+  if( direct ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  else {
+    if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
+    memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
+    memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  }
   hipError_t e;
   /* the slot's CU group only while another ring batch is in flight (a
      lone batch runs faster spread over the whole device: depth-1 p50
@@ -431,7 +508,12 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
       if( &g->slot[s] != sl && g->slot[s].ticket && hipEventQuery( g->slot[s].done ) == hipErrorNotReady ) others = 1;
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
-  if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
+  if( direct ) {
+    if( (e = hipMemcpyAsync( sl->d_blob, blob, blob_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
+      return fd_gpu_fail( "H2D blob (registered)", e );
+    if( (e = hipMemcpyAsync( sl->d_blob + doff, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
+      return fd_gpu_fail( "H2D desc", e );
+  } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
   if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )

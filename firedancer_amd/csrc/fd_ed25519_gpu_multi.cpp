@@ -3,39 +3,50 @@
 
    Signatures are independent, so a batch shards into contiguous index
    ranges, one per engine: nothing is reduced and no collective runs
-   between devices (xGMI stays idle).  Each engine gets only the blob
-   bytes its shard references (txn payloads are packed in index order,
-   so a shard's span is ~1/N of the blob), staged straight into that
-   engine's pinned ring slot and verified on its own host thread; the
-   per-signature codes land in the caller's out[] at their own indices
-   (the host-side gather), and fd_ed25519_codes_to_bitmap packs an
-   accept bitmap from them. */
+   between devices (xGMI stays idle).  Each shard is cut into chunks that
+   fit its engine and handed to that engine's feeder thread
+   (fd_ed25519_gpu_feeder.cpp: pinned to the GPU's NUMA node, whole ring
+   in flight: staging copy of chunk k+1 overlapping chunk k's transfers
+   and kernels); a chunk moves only the blob bytes it references (txn
+   payloads are packed in index order, so a shard's span is ~1/N of the
+   blob).  The per-signature codes land in the caller's out[] at their
+   own indices (the host-side gather), and fd_ed25519_codes_to_bitmap
+   packs an accept bitmap from them. */
 
 #include <string.h>
-#include <thread>
 #include <vector>
 #include "fd_ed25519_gpu.h"
 
 #define FD_EXPORT extern "C" __attribute__((visibility("default")))
 
 struct fd_ed25519_gpu_multi {
-  std::vector<fd_ed25519_gpu_t *> eng;
+  std::vector<fd_ed25519_gpu_t *>        eng;
+  std::vector<fd_ed25519_gpu_feeder_t *> feed;
 };
 
-FD_EXPORT fd_ed25519_gpu_multi_t * fd_ed25519_gpu_multi_new( int const * devices, int ndev,
-                                                             unsigned long max_sigs, unsigned long max_blob ) {
+FD_EXPORT fd_ed25519_gpu_multi_t * fd_ed25519_gpu_multi_new_ex( int const * devices, int ndev, unsigned long max_sigs,
+                                                                unsigned long max_blob, int depth ) {
   if( !devices || ndev < 1 || ndev > 64 ) return NULL;
   fd_ed25519_gpu_multi_t * m = new fd_ed25519_gpu_multi_t();
   for( int i=0; i<ndev; i++ ) {
-    fd_ed25519_gpu_t * g = fd_ed25519_gpu_new( devices[i], max_sigs, max_blob );
+    fd_ed25519_gpu_t * g = fd_ed25519_gpu_new_ex( devices[i], max_sigs, max_blob, depth );
     if( !g ) { fd_ed25519_gpu_multi_delete( m ); return NULL; }
     m->eng.push_back( g );
+    fd_ed25519_gpu_feeder_t * f = fd_ed25519_gpu_feeder_new( g, 1 );
+    if( !f ) { fd_ed25519_gpu_multi_delete( m ); return NULL; }
+    m->feed.push_back( f );
   }
   return m;
 }
 
+FD_EXPORT fd_ed25519_gpu_multi_t * fd_ed25519_gpu_multi_new( int const * devices, int ndev,
+                                                             unsigned long max_sigs, unsigned long max_blob ) {
+  return fd_ed25519_gpu_multi_new_ex( devices, ndev, max_sigs, max_blob, 3 );
+}
+
 FD_EXPORT void fd_ed25519_gpu_multi_delete( fd_ed25519_gpu_multi_t * m ) {
   if( !m ) return;
+  for( fd_ed25519_gpu_feeder_t * f : m->feed ) fd_ed25519_gpu_feeder_delete( f );   /* drain first */
   for( fd_ed25519_gpu_t * g : m->eng ) fd_ed25519_gpu_delete( g );
   delete m;
 }
@@ -45,19 +56,21 @@ FD_EXPORT int fd_ed25519_gpu_multi_cnt( fd_ed25519_gpu_multi_t const * m ) { ret
 FD_EXPORT fd_ed25519_gpu_t * fd_ed25519_gpu_multi_engine( fd_ed25519_gpu_multi_t * m, int i ) {
   return ( m && i >= 0 && i < (int)m->eng.size() ) ? m->eng[i] : NULL;
 }
+FD_EXPORT fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_multi_feeder( fd_ed25519_gpu_multi_t * m, int i ) {
+  return ( m && i >= 0 && i < (int)m->feed.size() ) ? m->feed[i] : NULL;
+}
 
 static inline int fd_mdesc_ok( fd_ed25519_gpu_desc_t const * d, unsigned long blob_sz ) {
   return (unsigned long)d->sig_off + 64UL <= blob_sz && (unsigned long)d->pub_off + 32UL <= blob_sz
       && (unsigned long)d->msg_off + (unsigned long)d->msg_sz <= blob_sz;
 }
 
-/* verify descs [lo,hi) on one engine, in chunks that fit its capacity */
-static int fd_multi_shard( fd_ed25519_gpu_t * g, unsigned long lo, unsigned long hi, uint8_t const * blob,
-                           unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, int * out ) {
-  unsigned long max_sigs = fd_ed25519_gpu_max_sigs( g ), max_blob = fd_ed25519_gpu_max_blob( g );
+/* cut descs [lo,hi) into chunks whose signature count and referenced byte
+   span fit one engine batch: appends chunk end indices to ends */
+static int fd_multi_chunks( unsigned long lo, unsigned long hi, fd_ed25519_gpu_desc_t const * desc, unsigned long blob_sz,
+                            unsigned long max_sigs, unsigned long max_blob, std::vector<unsigned long> & ends ) {
   unsigned long k = lo;
   while( k < hi ) {
-    /* grow the chunk while its referenced byte span fits the engine */
     unsigned long b0 = ~0UL, b1 = 0, e = k;
     while( e < hi && e - k < max_sigs ) {
       fd_ed25519_gpu_desc_t const * d = &desc[e];
@@ -74,22 +87,7 @@ static int fd_multi_shard( fd_ed25519_gpu_t * g, unsigned long lo, unsigned long
       e++;
     }
     if( e == k ) return FD_ED25519_ERR_ARG;          /* one signature spans more than an engine blob */
-    if( b0 == ~0UL ) { b0 = 0; b1 = 0; }             /* every descriptor in the chunk is malformed */
-    void * sb; fd_ed25519_gpu_desc_t * sd;
-    if( fd_ed25519_gpu_stage( g, &sb, &sd ) ) return FD_ED25519_ERR_GPU;
-    memcpy( sb, blob + b0, b1 - b0 );
-    for( unsigned long i=k; i<e; i++ ) {
-      fd_ed25519_gpu_desc_t d = desc[i];
-      if( fd_mdesc_ok( &d, blob_sz ) ) { d.sig_off -= (uint32_t)b0; d.pub_off -= (uint32_t)b0; d.msg_off -= (uint32_t)b0; }
-      else { d.sig_off = d.pub_off = d.msg_off = 0xffffffffu; d.msg_sz = 0; }   /* reported as ERR_ARG */
-      sd[i-k] = d;
-    }
-    unsigned long ticket;
-    int err = fd_ed25519_gpu_submit( g, e - k, sb, b1 - b0, sd, &ticket );
-    if( err ) { fd_ed25519_gpu_unstage( g, sb ); return err; }
-    int r = fd_ed25519_gpu_poll( g, ticket, out + k, 1 );
-    if( r != 1 ) return FD_ED25519_ERR_GPU;
-    for( unsigned long i=k; i<e; i++ ) if( !fd_mdesc_ok( &desc[i], blob_sz ) ) out[i] = FD_ED25519_ERR_ARG;
+    ends.push_back( e );
     k = e;
   }
   return 0;
@@ -100,18 +98,47 @@ FD_EXPORT int fd_ed25519_gpu_multi_verify_packed( fd_ed25519_gpu_multi_t * m, un
   if( !m || (n && (!desc || !out)) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
   int nd = (int)m->eng.size();
-  std::vector<int> err( nd, 0 );
-  std::vector<std::thread> th;
+  /* every shard's chunks first (an ERR_ARG writes nothing) */
+  std::vector<std::vector<unsigned long>> ends( nd );
+  std::vector<unsigned long> los( nd );
   for( int d=0; d<nd; d++ ) {
     unsigned long lo = n * (unsigned long)d / (unsigned long)nd, hi = n * (unsigned long)(d+1) / (unsigned long)nd;
-    if( lo == hi ) continue;
-    th.emplace_back( [&, d, lo, hi]() {
-      err[d] = fd_multi_shard( m->eng[d], lo, hi, (uint8_t const *)blob, blob_sz, desc, out );
-    } );
+    los[d] = lo;
+    int err = fd_multi_chunks( lo, hi, desc, blob_sz, fd_ed25519_gpu_max_sigs( m->eng[d] ), fd_ed25519_gpu_max_blob( m->eng[d] ), ends[d] );
+    if( err ) return err;
   }
-  for( std::thread & t : th ) t.join();
-  for( int d=0; d<nd; d++ ) if( err[d] ) return err[d];
-  return 0;
+  /* each device's feeder gets its chunks in order; all devices at once */
+  std::vector<std::vector<fd_ed25519_gpu_job_t>> jobs( nd );
+  for( int d=0; d<nd; d++ ) {
+    jobs[d].resize( ends[d].size() );
+    unsigned long k = los[d];
+    for( size_t c=0; c<ends[d].size(); c++ ) {
+      fd_ed25519_gpu_job_t * j = &jobs[d][c];
+      memset( j, 0, sizeof(*j) );
+      j->n = ends[d][c] - k; j->blob = blob; j->blob_sz = blob_sz; j->desc = desc + k; j->out = out + k;
+      k = ends[d][c];
+    }
+  }
+  int err = 0;
+  /* push round-robin across devices so every feeder starts at once */
+  size_t most = 0;
+  for( int d=0; d<nd; d++ ) if( jobs[d].size() > most ) most = jobs[d].size();
+  std::vector<std::vector<int>> pushed( nd );
+  for( size_t c=0; c<most; c++ )
+    for( int d=0; d<nd; d++ )
+      if( c < jobs[d].size() ) {
+        int e = fd_ed25519_gpu_feeder_push( m->feed[d], &jobs[d][c] );
+        pushed[d].push_back( !e );
+        if( e && !err ) err = e;
+      }
+  /* wait for everything pushed (the jobs live on this stack frame) */
+  for( int d=0; d<nd; d++ )
+    for( size_t c=0; c<jobs[d].size(); c++ ) {
+      if( !pushed[d][c] ) continue;
+      int e = fd_ed25519_gpu_job_wait( &jobs[d][c], -1 );
+      if( e && !err ) err = e;
+    }
+  return err;
 }
 
 FD_EXPORT void fd_ed25519_codes_to_bitmap( unsigned long n, int const * codes, uint8_t * bitmap ) {

@@ -177,6 +177,23 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 
+/* CU groups of the ring: slot s runs small batches (<= 64 signatures per
+   group CU) on the CUs c with c mod groups == s mod groups while another
+   ring batch is in flight, so concurrent small batches do not share SIMDs
+   (every group spans all XCDs).  Default min(depth, 4); 1 = none.  The
+   ring must be idle (nothing submitted or staged). */
+int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * gpu, int groups );
+int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
+
+/* Register a host region the ring may DMA from in place
+   (hipHostRegister; call before sandboxing, e.g. on the tile's input
+   dcache).  A submitted blob lying inside a registered region is copied
+   to the device straight from the caller's bytes -- no staging memcpy --
+   so those bytes must stay unchanged until the batch is polled.  Up to
+   16 regions per engine. */
+int fd_ed25519_gpu_register  ( fd_ed25519_gpu_t * gpu, void * host, unsigned long sz );
+int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * gpu, void * host );
+
 /* Bound on every blocking wait of the engine, in ns (default 10 s; < 0:
    unbounded).  A wait that exceeds it returns FD_ED25519_ERR_GPU instead
    of hanging the caller on a wedged queue (as the reference's
@@ -273,20 +290,65 @@ fd_ed25519_gpu_t * fd_ed25519_gpu_default( void );
 /* Number of usable gfx950 devices visible to this process. */
 int fd_ed25519_gpu_device_cnt( void );
 
+/* ---- Per-GPU feeder ------------------------------
+
+   One host thread per engine, pinned to the CPUs of the GPU's NUMA node
+   (pin_numa), keeping the engine's ring full: a pushed job's descriptors
+   are verified against its blob; the feeder copies the byte span they
+   reference into a free ring slot (no copy for a registered region),
+   rebases the descriptors, submits, and collects completed batches oldest
+   first while later ones are staged.  Jobs complete in push order.
+
+   A job is owned by the caller; blob, desc and out must stay valid until
+   its state is nonzero: 1 = codes in out[0..n), < 0 = FD_ED25519_ERR_*
+   (nothing written).  t_*_ns are CLOCK_MONOTONIC stamps of push, submit
+   (H2D enqueued) and completion (codes on the host). */
+
+typedef struct fd_ed25519_gpu_job {
+  unsigned long                 n;
+  void const *                  blob;
+  unsigned long                 blob_sz;
+  fd_ed25519_gpu_desc_t const * desc;
+  int *                         out;
+  int                           state;     /* written by the feeder (atomic release) */
+  unsigned long                 t_push_ns, t_submit_ns, t_done_ns;
+} fd_ed25519_gpu_job_t;
+
+typedef struct fd_ed25519_gpu_feeder fd_ed25519_gpu_feeder_t;
+
+fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_feeder_new( fd_ed25519_gpu_t * gpu, int pin_numa );
+/* Drains: every pushed job completes before the thread exits. */
+void fd_ed25519_gpu_feeder_delete   ( fd_ed25519_gpu_feeder_t * feeder );
+/* NUMA node the feeder thread is pinned to, -1 if none. */
+int  fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * feeder );
+/* Queue a job (n <= the engine's max_sigs; the referenced span must fit
+   its max_blob, else the job completes with FD_ED25519_ERR_ARG). */
+int  fd_ed25519_gpu_feeder_push     ( fd_ed25519_gpu_feeder_t * feeder, fd_ed25519_gpu_job_t * job );
+/* Wait for a job: 0 done, its error code, or FD_ED25519_ERR_GPU after
+   timeout_ns (< 0: no bound). */
+int  fd_ed25519_gpu_job_wait        ( fd_ed25519_gpu_job_t const * job, long timeout_ns );
+
 /* ---- Multi-device --------------------------------
 
    Several engines fed by one host: a batch is sharded into contiguous
    signature ranges, one per engine (ndev entries of devices[], repeats
-   allowed), each engine receives only the blob bytes its shard
-   references, shards run concurrently on per-device host threads, and
-   the codes are gathered into out[] in index order.  No collective: the
-   path has no exchange step.  Same codes and error behaviour as
-   fd_ed25519_gpu_verify_packed. */
+   allowed), each cut into chunks that fit the engine; every engine has
+   its own feeder thread (pinned to its GPU's NUMA node) that keeps its
+   ring full with its chunks, each receiving only the blob bytes it
+   references, and the codes land in out[] in index order.  No
+   collective: the path has no exchange step.  Same codes and error
+   behaviour as fd_ed25519_gpu_verify_packed. */
 
 typedef struct fd_ed25519_gpu_multi fd_ed25519_gpu_multi_t;
 
 fd_ed25519_gpu_multi_t *
 fd_ed25519_gpu_multi_new( int const * devices, int ndev, unsigned long max_sigs, unsigned long max_blob );
+
+/* As above with each engine's ring depth (1..8). */
+fd_ed25519_gpu_multi_t *
+fd_ed25519_gpu_multi_new_ex( int const * devices, int ndev, unsigned long max_sigs, unsigned long max_blob, int depth );
+
+fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_multi_feeder( fd_ed25519_gpu_multi_t * multi, int idx );
 
 void               fd_ed25519_gpu_multi_delete( fd_ed25519_gpu_multi_t * multi );
 int                fd_ed25519_gpu_multi_cnt   ( fd_ed25519_gpu_multi_t const * multi );

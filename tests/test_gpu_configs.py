@@ -204,3 +204,65 @@ def test_verify_dev_orders_calls_across_streams(engine, ref):
     torch.cuda.synchronize()
     for (_, _, out), e in zip(keep, exps):
         _check(out.cpu().numpy(), e)
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_feeder_stream_vs_reference(ref, register):
+    """the per-GPU feeder (fd_ed25519_gpu_feeder) keeps a depth-6 ring full
+    with 24 jobs of 1..4096 adversarial txn-shaped signatures (copied into
+    the pinned ring, or DMA'd in place from a registered blob); every code
+    equals the reference's, jobs complete in push order"""
+    b = corpus.adversarial_txns(4096 * 6, seed=123, invalid_frac=0.15)
+    exp = oracle_batch(ref, b)
+    e = fa.Engine(0, 4096, 8 << 20, depth=6)
+    try:
+        e.cu_groups = 3
+        assert e.cu_groups == 3
+        if register:
+            e.register(b.blob)
+        f = fa.Feeder(e)
+        rng = np.random.default_rng(5)
+        spans = []
+        for _ in range(24):
+            n = int(rng.integers(1, 4097))
+            lo = int(rng.integers(0, len(b) - n))
+            spans.append((lo, n))
+        jobs, outs = [], []
+        for lo, n in spans:
+            d = np.ascontiguousarray(b.desc[lo:lo + n])
+            o = np.full(n, 99, np.int32)
+            jobs.append((f.push(b.blob, d, o), lo, n))
+            outs.append(o)
+        last = 0
+        for (j, lo, n), o in zip(jobs, outs):
+            f.wait(j)
+            assert j.t_done_ns >= last
+            last = j.t_done_ns
+            _check(o, exp[lo:lo + n], None)
+        f.close()
+    finally:
+        e.close()
+
+
+def test_cu_groups_depth8_ring_vs_reference(ref):
+    """ring depth 8 over 4 CU groups, 4096-signature batches kept in flight
+    through submit/poll; codes against the reference"""
+    b = corpus.adversarial(4096 * 2, 128, seed=321, invalid_frac=0.2)
+    exp = oracle_batch(ref, b)
+    e = fa.Engine(0, 4096, 4 << 20, depth=8)
+    try:
+        e.cu_groups = 4
+        halves = [(np.ascontiguousarray(b.desc[h * 4096:(h + 1) * 4096]), exp[h * 4096:(h + 1) * 4096]) for h in range(2)]
+        inflight, out = [], np.zeros(4096, np.int32)
+        for k in range(24):
+            if len(inflight) == e.depth:
+                t, x = inflight.pop(0)
+                assert e.poll(t, out, block=True)
+                _check(out, x)
+            d, x = halves[k % 2]
+            inflight.append((e.submit(b.blob, d), x))
+        for t, x in inflight:
+            assert e.poll(t, out, block=True)
+            _check(out, x)
+    finally:
+        e.close()
