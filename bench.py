@@ -335,7 +335,7 @@ def main():
         dist.destroy_process_group()
 
 
-def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7):
+def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None):
     """C2 at its own granularity: nb 4096-signature batches streamed through
     one engine's pinned ring by its per-GPU feeder thread
     (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
@@ -348,6 +348,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
     try:
         if groups:
             eng.cu_groups = groups
+        if quad2 is not None:
+            eng.quad2 = quad2
         if register:
             eng.register(base.blob)
         feeder = fa.Feeder(eng)
@@ -381,7 +383,7 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         lat = np.array(lat[W:]) if len(lat) > 2 * W else np.array(lat)
         qlat = np.array(qlat[W:]) if len(qlat) > 2 * W else np.array(qlat)
         return {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
-                "cu_groups": eng.cu_groups, "registered_source": bool(register),
+                "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "registered_source": bool(register),
                 "feeder_numa_node": numa,
                 "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
                 "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),

@@ -34,6 +34,7 @@
 #include <thread>
 #include <vector>
 #include "fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_desc.h"
 
 #define FD_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -101,30 +102,11 @@ static void fd_job_finish( fd_ed25519_gpu_job_t * j, int state ) {
 
 /* stage + submit one job; 1 submitted, 0 ring full (retry later), < 0 the job failed (finished) */
 static int fd_feeder_submit( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
-  fd_ed25519_gpu_desc_t const * d = j->desc;
-  unsigned long n = j->n, b0 = ~0UL, b1 = 0UL;
-  for( unsigned long i=0; i<n; i++ ) {
-    unsigned long lo = d[i].sig_off, hi = (unsigned long)d[i].sig_off + 64UL;
-    if( (unsigned long)d[i].pub_off + 32UL > j->blob_sz || hi > j->blob_sz
-     || (unsigned long)d[i].msg_off + (unsigned long)d[i].msg_sz > j->blob_sz ) continue;   /* ERR_ARG on the device */
-    if( d[i].pub_off < lo ) lo = d[i].pub_off;
-    if( d[i].msg_off < lo ) lo = d[i].msg_off;
-    if( (unsigned long)d[i].pub_off + 32UL > hi ) hi = (unsigned long)d[i].pub_off + 32UL;
-    if( (unsigned long)d[i].msg_off + d[i].msg_sz > hi ) hi = (unsigned long)d[i].msg_off + d[i].msg_sz;
-    if( lo < b0 ) b0 = lo;
-    if( hi > b1 ) b1 = hi;
-  }
-  if( b0 == ~0UL ) { b0 = 0UL; b1 = 0UL; }
+  unsigned long n = j->n, b0, b1;
+  fd_ed25519_desc_span( n, j->desc, j->blob_sz, &b0, &b1 );
   if( b1 - b0 > f->max_blob ) { fd_job_finish( j, FD_ED25519_ERR_ARG ); return -1; }
   fd_ed25519_gpu_desc_t * rd = f->rebased.data();
-  for( unsigned long i=0; i<n; i++ ) {
-    fd_ed25519_gpu_desc_t x = d[i];
-    if( (unsigned long)x.sig_off + 64UL <= j->blob_sz && (unsigned long)x.pub_off + 32UL <= j->blob_sz
-     && (unsigned long)x.msg_off + (unsigned long)x.msg_sz <= j->blob_sz ) {
-      x.sig_off -= (uint32_t)b0; x.pub_off -= (uint32_t)b0; x.msg_off -= (uint32_t)b0;
-    } else { x.sig_off = x.pub_off = x.msg_off = 0xffffffffu; x.msg_sz = 0; }   /* stays out of bounds */
-    rd[i] = x;
-  }
+  fd_ed25519_desc_rebase( n, j->desc, j->blob_sz, b0, rd );
   unsigned long ticket = 0;
   int err = fd_ed25519_gpu_submit( f->gpu, n, (uint8_t const *)j->blob + b0, b1 - b0, rd, &ticket );
   if( err == FD_ED25519_ERR_ARG ) return 0;                       /* every slot in flight */

@@ -138,6 +138,7 @@ struct fd_ed25519_gpu {
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
+  int           quad2;    /* FD_ED25519_GPU_QUAD2_*: when small batches take the 2-waves/SIMD quad DSM */
   int           ncu;
   struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none) */
@@ -227,6 +228,8 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   g->timeout_ns = FD_WAIT_TIMEOUT_NS_DEFAULT;
+  g->quad2 = FD_ED25519_GPU_QUAD2_RING;
+  { char const * q2 = getenv( "FD_ED25519_GPU_QUAD2" ); if( q2 ) g->quad2 = atoi( q2 ); }   /* experiments */
   /* a slot's pinned and device blob buffers also hold the batch's
      descriptors, 16-aligned after the padded blob, so a batch is ONE H2D
      copy (a second small copy costs ~17 us of a ~0.75 ms 4096-signature
@@ -336,6 +339,14 @@ extern "C" int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * g, int groups ) 
   return 0;
 }
 extern "C" int fd_ed25519_gpu_cu_groups( fd_ed25519_gpu_t const * g ) { return g ? g->groups : 0; }
+
+extern "C" int fd_ed25519_gpu_set_quad2( fd_ed25519_gpu_t * g, int policy ) {
+  if( !g || policy < FD_ED25519_GPU_QUAD2_NEVER || policy > FD_ED25519_GPU_QUAD2_ALWAYS ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  g->quad2 = policy;
+  return 0;
+}
+extern "C" int fd_ed25519_gpu_quad2( fd_ed25519_gpu_t const * g ) { return g ? g->quad2 : -1; }
 
 /* Host regions the ring may DMA from directly (no staging copy): a batch
    whose blob lies inside one goes H2D straight from the caller's bytes
@@ -448,7 +459,8 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   if( (e = hipStreamWaitEvent( st, g->dev_done, 0 )) != hipSuccess ) return fd_gpu_fail( "hipStreamWaitEvent", e );
   e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work, (int32_t *)d_out, st, ev,
-                                   g->mode, g->pool_min, g->quad_max );
+                                   g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0),
+                                   g->pool_min, g->quad_max );
   if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
   if( (e = hipEventRecord( g->dev_done, st )) != hipSuccess ) return fd_gpu_fail( "hipEventRecord", e );
   return 0;
@@ -484,6 +496,7 @@ extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_
    kernels, copy-out on the slot's stream.  Descriptors are copied as
    given: the device checks each against blob_sz and reports an
    out-of-bounds one as FD_ED25519_ERR_ARG (fd_k_prep). */
+static int fd_ring_busy( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot const * sl );
 static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
                              unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, hipStream_t * used ) {
   unsigned long doff = fd_desc_off( blob_sz );
@@ -502,12 +515,12 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   /* the slot's CU group only while another ring batch is in flight (a
      lone batch runs faster spread over the whole device: depth-1 p50
      0.755 ms there vs 0.80 ms on a third of the CUs) */
-  int others = 0;
-  if( sl->mstream && n <= g->mask_max )
-    for( int s=0; s<g->depth; s++ )
-      if( &g->slot[s] != sl && g->slot[s].ticket && hipEventQuery( g->slot[s].done ) == hipErrorNotReady ) others = 1;
+  int others = sl->mstream && n <= g->mask_max && fd_ring_busy( g, sl );
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
+  /* several ring batches in flight: the quad DSM at two waves per SIMD */
+  int lflags = ( g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS || (g->quad2 == FD_ED25519_GPU_QUAD2_RING && fd_ring_busy( g, sl )) )
+             ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0;
   if( direct ) {
     if( (e = hipMemcpyAsync( sl->d_blob, blob, blob_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D blob (registered)", e );
@@ -516,12 +529,19 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode | lflags, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
   if( (e = hipEventRecord( sl->done, st )) != hipSuccess ) return fd_gpu_fail( "event", e );
   sl->n = n;
+  return 0;
+}
+
+/* another ring batch still in flight? */
+static int fd_ring_busy( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot const * sl ) {
+  for( int s=0; s<g->depth; s++ )
+    if( &g->slot[s] != sl && g->slot[s].ticket && hipEventQuery( g->slot[s].done ) == hipErrorNotReady ) return 1;
   return 0;
 }
 

@@ -639,12 +639,26 @@ struct fd_quad_lds {
   int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
   uint8_t ops[FD_OPS_MAX][FD_QSIGS];
 };
+/* the two-waves-per-SIMD form: Ai lanes unpadded (40 B), nothing else in
+   LDS (op bytes and Bi come from global memory, loaded a step ahead) --
+   20 KiB per wave, 8 waves per CU */
+#define FD_QLANE 10
+struct fd_quad_lds2 {
+  int32_t tab[FD_QSIGS][8*4*FD_QLANE];
+};
 
 FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   int4 * q = (int4 *)p;
   q[0] = make_int4( v.v[0], v.v[1], v.v[2], v.v[3] );
   q[1] = make_int4( v.v[4], v.v[5], v.v[6], v.v[7] );
   q[2] = make_int4( v.v[8], v.v[9], 0, 0 );
+}
+template<int LITE> FD_QDEV void fd_q_tab_store_t( int32_t * p, fe const & v ) {
+  if constexpr( LITE ) {
+    int2 * q = (int2 *)p;
+#pragma unroll
+    for( int k=0; k<5; k++ ) q[k] = make_int2( v.v[2*k], v.v[2*k+1] );
+  } else fd_q_tab_store( p, v );
 }
 
 #ifndef FD_QUAD_ILP
@@ -661,11 +675,10 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
 #define FD_QMUL fd_fe_mul
 #endif
 
-extern "C" __global__ void __launch_bounds__(64)
-fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
-               int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-               int32_t * __restrict__ out, int strict ) {
-  __shared__ __attribute__((aligned(16))) fd_quad_lds L;
+template<int LITE, typename LDS>
+FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+                           int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+                           int32_t * __restrict__ out, int strict, LDS & L ) {
   uint32_t lane = threadIdx.x;
   uint32_t q    = lane & 3u, ls = lane >> 2;
   uint64_t sig0 = (uint64_t)blockIdx.x * FD_QSIGS;
@@ -698,11 +711,13 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   /* op streams of the wave's 16 signatures -> LDS (rows from the wave's
      first op on) */
   int t0 = fd_wave_min( start );
-  for( int t=t0+(int)(lane>>4); t<FD_OPS_MAX; t+=4 ) {
-    uint64_t gs = sig0 + (lane & 15u);
-    L.ops[t][lane & 15u] = gs < n ? ops[(uint64_t)t*n + gs] : (uint8_t)0;
+  if constexpr( !LITE ) {
+    for( int t=t0+(int)(lane>>4); t<FD_OPS_MAX; t+=4 ) {
+      uint64_t gs = sig0 + (lane & 15u);
+      L.ops[t][lane & 15u] = gs < n ? ops[(uint64_t)t*n + gs] : (uint8_t)0;
+    }
+    for( int k=lane; k<8*FD_TAB_ENTRY; k+=64 ) L.tab[FD_QSIGS][k] = fd_gpu_bi_tab[k];
   }
-  for( int k=lane; k<8*FD_TAB_ENTRY; k+=64 ) L.tab[FD_QSIGS][k] = fd_gpu_bi_tab[k];
 
   /* per-lane constant masks */
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
@@ -712,9 +727,10 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   fe one; fd_fe_set( one, 1 );
   fe d111 = q==3u ? FD_GPU_D2 : one;
   int32_t * tab_s = L.tab[ls];
+  int const lstride = LITE ? FD_QLANE : FD_TAB_LANE, estride = 4*lstride;
   fe vu, vt, f, g;
   FD_QMUL( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
-  fd_q_tab_store( tab_s + q*FD_TAB_LANE, vu );
+  fd_q_tab_store_t<LITE>( tab_s + q*lstride, vu );
   {  /* v_p2_dbl: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)), squarings as f*f, Z*(2Z) */
     fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
 #pragma unroll
@@ -733,7 +749,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
     FD_QMUL( vt, f, g );
     FD_QMUL( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
-    fd_q_tab_store( tab_s + (e+1)*FD_TAB_ENTRY + q*FD_TAB_LANE, vu );
+    fd_q_tab_store_t<LITE>( tab_s + (e+1)*estride + q*lstride, vu );
   }
   __syncthreads();
 
@@ -742,14 +758,36 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
      [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
+  /* LITE: this signature's op byte for the next step, loaded a step ahead */
+  uint8_t const * ops_i = ops + ii;
+  int opn = 0;
+  if constexpr( LITE ) opn = (t0 >= start && t0 < FD_OPS_MAX) ? (int)ops_i[(uint64_t)t0*n] : 0;
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
-    int op = t >= start ? (int)L.ops[t][ls] : 0;
+    int op;
+    if constexpr( LITE ) {
+      op = opn;
+      opn = (t + 1 >= start && t + 1 < FD_OPS_MAX) ? (int)ops_i[(uint64_t)(t + 1)*n] : 0;
+    } else op = t >= start ? (int)L.ops[t][ls] : 0;
     uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
     uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
     uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
-    int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
-    int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
+    int32_t E[10];
+    if constexpr( LITE ) {
+      if( op & 0x40 ) {   /* Bi from global memory (1.5 KiB, cache resident), padded lanes */
+        int4 const * ent = (int4 const *)(fd_gpu_bi_tab + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE);
+        int4 ea = ent[0], eb = ent[1]; int2 ec = *(int2 const *)(ent + 2);
+        E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
+      } else {
+        int2 const * ent = (int2 const *)(tab_s + (op & 7)*estride + idx*lstride);
+#pragma unroll
+        for( int k=0; k<5; k++ ) { int2 x = ent[k]; E[2*k] = x.x; E[2*k+1] = x.y; }
+      }
+    } else {
+      int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
+      int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
+      E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
+    }
 
     fe C;
     fd_fe_qperm<FD_QP(2,1,0,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
@@ -760,7 +798,6 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     fd_fe_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fe_qperm<FD_QP(2,2,2,2)>( w, C );
     uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
     uint32_t gs = (q==1u && !add) ? 1u : 0u;
-    int32_t E[10] = { ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y };
 #pragma unroll
     for( int k=0; k<10; k++ ) {
       uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_qterm( (uint32_t)w.v[k], mW, mq2 ) );
@@ -803,6 +840,23 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   int eq1 = fd_qperm<FD_QP(1,1,1,1)>( eq );
   if( code == FD_ST_PENDING ) code = (eq & eq1) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   if( live && q == 0u ) out[i] = code;
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+               int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+               int32_t * __restrict__ out, int strict ) {
+  __shared__ __attribute__((aligned(16))) fd_quad_lds L;
+  fd_quad_body<0>( n, status, pstat, pts, ops, op_start, out, strict, L );
+}
+
+/* two waves per SIMD (streaming: several ring batches in flight) */
+extern "C" __global__ void __launch_bounds__(64, 2)
+fd_k_dsm_quad2( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+                int32_t * __restrict__ out, int strict ) {
+  __shared__ __attribute__((aligned(16))) fd_quad_lds2 L;
+  fd_quad_body<1>( n, status, pstat, pts, ops, op_start, out, strict, L );
 }
 
 /* ------------------------------------------------------------------ */
@@ -1220,8 +1274,10 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                                     hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
+  int flags = mode & ~0xff; mode &= 0xff;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
+  mode |= flags;
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
@@ -1254,8 +1310,12 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
   } else if( quad ) {
     if( ev ) hipEventRecord( ev[3], stream );
-    hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
-                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
+    if( mode & FD_ED25519_GPU_LAUNCH_QUAD2 )
+      hipLaunchKernelGGL( fd_k_dsm_quad2, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
+                          n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
+    else
+      hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
+                          n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
     if( ev ) hipEventRecord( ev[4], stream );
   } else {
     if( ev ) hipEventRecord( ev[3], stream );

@@ -16,6 +16,7 @@
 #include <string.h>
 #include <vector>
 #include "fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_desc.h"
 
 #define FD_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -60,32 +61,13 @@ FD_EXPORT fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_multi_feeder( fd_ed25519_gpu_
   return ( m && i >= 0 && i < (int)m->feed.size() ) ? m->feed[i] : NULL;
 }
 
-static inline int fd_mdesc_ok( fd_ed25519_gpu_desc_t const * d, unsigned long blob_sz ) {
-  return (unsigned long)d->sig_off + 64UL <= blob_sz && (unsigned long)d->pub_off + 32UL <= blob_sz
-      && (unsigned long)d->msg_off + (unsigned long)d->msg_sz <= blob_sz;
-}
-
 /* cut descs [lo,hi) into chunks whose signature count and referenced byte
    span fit one engine batch: appends chunk end indices to ends */
 static int fd_multi_chunks( unsigned long lo, unsigned long hi, fd_ed25519_gpu_desc_t const * desc, unsigned long blob_sz,
                             unsigned long max_sigs, unsigned long max_blob, std::vector<unsigned long> & ends ) {
   unsigned long k = lo;
   while( k < hi ) {
-    unsigned long b0 = ~0UL, b1 = 0, e = k;
-    while( e < hi && e - k < max_sigs ) {
-      fd_ed25519_gpu_desc_t const * d = &desc[e];
-      if( fd_mdesc_ok( d, blob_sz ) ) {
-        unsigned long lo_ = d->sig_off, hi_ = (unsigned long)d->sig_off + 64UL;
-        if( d->pub_off < lo_ ) lo_ = d->pub_off;
-        if( d->msg_off < lo_ ) lo_ = d->msg_off;
-        if( (unsigned long)d->pub_off + 32UL > hi_ ) hi_ = (unsigned long)d->pub_off + 32UL;
-        if( (unsigned long)d->msg_off + d->msg_sz > hi_ ) hi_ = (unsigned long)d->msg_off + d->msg_sz;
-        unsigned long nb0 = lo_ < b0 ? lo_ : b0, nb1 = hi_ > b1 ? hi_ : b1;
-        if( nb1 - nb0 > max_blob ) break;
-        b0 = nb0; b1 = nb1;
-      }
-      e++;
-    }
+    unsigned long e = fd_ed25519_desc_chunk( k, hi, desc, blob_sz, max_sigs, max_blob );
     if( e == k ) return FD_ED25519_ERR_ARG;          /* one signature spans more than an engine blob */
     ends.push_back( e );
     k = e;

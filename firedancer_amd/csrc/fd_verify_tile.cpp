@@ -187,7 +187,7 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
     }
     /* every ring slot busy: back-pressure until the oldest batch lands */
     if( t->inflight.empty() ) return FD_ED25519_ERR_GPU;
-    t->diag[ FD_VERIFY_TILE_DIAG_BACKP_CNT ]++;
+    t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
     int err = fd_vt_drain( t, 1 );
     if( err ) return err;
   }
@@ -302,5 +302,6 @@ FD_EXPORT int fd_verify_tile_service( fd_verify_tile_t * t, int flush ) {
 
 FD_EXPORT void fd_verify_tile_diag( fd_verify_tile_t const * t, unsigned long * diag ) {
   memcpy( diag, t->diag, sizeof(t->diag) );
-  diag[ FD_VERIFY_TILE_DIAG_IN_BACKP ] = 0UL;
+  diag[ FD_VERIFY_TILE_DIAG_IN_BACKP  ] = 0UL;   /* flow control lives in the task's run loop */
+  diag[ FD_VERIFY_TILE_DIAG_BACKP_CNT ] = 0UL;
 }

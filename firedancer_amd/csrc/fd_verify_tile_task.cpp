@@ -1,0 +1,151 @@
+/* fd_verify_tile_task.cpp -- the GPU verify tile as a task with the
+   reference's tile shape (fd_frank_task_t, src/app/frank/fd_frank.h:29-45,
+   instance `verify` at src/app/frank/fd_frank_verify.c:207-211).
+
+   init (before the sandbox closes syscalls, fd_frank_verify.c:14-20):
+     creates ALL device state -- the engine (HIP runtime, device buffers,
+     pinned ring, streams) and the tile -- and reports the extended
+     seccomp allowlist and close_fd_start.
+   run (fd_frank_verify.c:22-205): the reference's loop with its
+     placeholder (:196-203) filled in:
+       housekeeping at a low rate (:143-182): heartbeat, diagnostics into
+         the cnc app region, cnc signal check (HALT -> drain, publish,
+         BOOT; anything else -> FAIL), flow-control credits and the
+         IN_BACKP / BACKP_CNT diagnostics, publish of completed batches;
+       backpressure (:185-194): no credits -> IN_BACKP = 1, BACKP_CNT++;
+       the frag path: next frag from the input -> fd_verify_tile_rx
+         (HA dedup, staging into the pinned ring, batch submit).
+   fini: drains and frees (the reference's tile process simply exits). */
+
+#include <linux/unistd.h>
+#include <string.h>
+#include <time.h>
+#include "fd_verify_tile.h"
+
+#define FD_EXPORT extern "C" __attribute__((visibility("default")))
+
+/* The reference tile's four (fd_frank_verify.c:7-12) plus what the HIP
+   runtime issues after init on the tile's hot path: ioctl (KFD/DRM event
+   waits and queue doorbells), mmap / munmap / mprotect / madvise (runtime
+   memory-pool growth), sched_yield (runtime spin-waits),
+   clock_nanosleep (glibc's nanosleep) and get_mempolicy (the runtime's
+   NUMA queries on the copy path).  Checked on an MI355X by
+   tests/test_verify_tile_task.py::test_task_under_seccomp (a seccomp
+   filter that allows exactly this list around the whole run loop). */
+static long const fd_vt_allow_syscalls[] = {
+  __NR_write,           /* logging */
+  __NR_futex,           /* logging; runtime locks */
+  __NR_fsync,           /* logging */
+  __NR_nanosleep,       /* tick calibration; bounded waits */
+  __NR_ioctl,           /* HIP: KFD / DRM */
+  __NR_mmap,            /* HIP: memory pools */
+  __NR_munmap,
+  __NR_mprotect,
+  __NR_madvise,
+  __NR_sched_yield,     /* HIP spin-waits */
+  __NR_clock_nanosleep, /* glibc nanosleep */
+  __NR_get_mempolicy,   /* HIP: NUMA placement queries on the copy path */
+};
+
+static long fd_vt_now( void ) {
+  struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t );
+  return (long)t.tv_sec * 1000000000L + (long)t.tv_nsec;
+}
+
+static void fd_vt_cnc_set( fd_verify_tile_cnc_t * cnc, unsigned long s ) {
+  __atomic_store_n( &cnc->signal, s, __ATOMIC_RELEASE );
+}
+static unsigned long fd_vt_cnc_query( fd_verify_tile_cnc_t const * cnc ) {
+  return __atomic_load_n( &cnc->signal, __ATOMIC_ACQUIRE );
+}
+
+static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
+  a->err = 0;
+  a->close_fd_start    = 4U;   /* stdin, stdout, stderr, logfile (fd_frank_verify.c:16) */
+  a->allow_syscalls_sz = (unsigned short)(sizeof(fd_vt_allow_syscalls) / sizeof(fd_vt_allow_syscalls[0]));
+  a->allow_syscalls    = fd_vt_allow_syscalls;
+  a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, a->depth ? a->depth : 3 );
+  a->tile = a->gpu ? fd_verify_tile_new( a->gpu, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+  if( !a->gpu || !a->tile ) {
+    a->err = FD_ED25519_ERR_GPU;
+    if( a->cnc ) fd_vt_cnc_set( a->cnc, FD_VERIFY_TILE_SIGNAL_FAIL );
+  }
+}
+
+static void fd_vt_diag_push( fd_verify_tile_args_t * a, int in_backp, unsigned long backp_cnt ) {
+  unsigned long d[ FD_VERIFY_TILE_DIAG_CNT ];
+  fd_verify_tile_diag( a->tile, d );
+  d[ FD_VERIFY_TILE_DIAG_IN_BACKP  ] = (unsigned long)in_backp;
+  d[ FD_VERIFY_TILE_DIAG_BACKP_CNT ] = backp_cnt;
+  for( unsigned long k=0; k<FD_VERIFY_TILE_DIAG_CNT; k++ ) __atomic_store_n( &a->cnc->diag[k], d[k], __ATOMIC_RELAXED );
+}
+
+static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
+  fd_verify_tile_cnc_t * cnc = a->cnc;
+  if( a->err || !cnc || !a->in ) { a->err = a->err ? a->err : FD_ED25519_ERR_ARG; if( cnc ) fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+  if( fd_vt_cnc_query( cnc ) != FD_VERIFY_TILE_SIGNAL_BOOT ) { a->err = FD_ED25519_ERR_ARG; fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+  int           in_backp  = 1;          /* as the reference tile boots (fd_frank_verify.c:46-52) */
+  unsigned long backp_cnt = 0UL;
+  unsigned long cr_avail  = 0UL;
+  long lazy = a->lazy_ns > 0 ? a->lazy_ns : 100000L;   /* 100 us housekeeping interval by default */
+  unsigned long rng = 0x9e3779b97f4a7c15UL ^ (unsigned long)a->device;
+  fd_vt_diag_push( a, in_backp, backp_cnt );
+  long now = fd_vt_now(), then = now;
+  fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_RUN );
+  for(;;) {
+    if( now - then >= 0L ) {
+      /* housekeeping (fd_frank_verify.c:143-182) */
+      __atomic_store_n( &cnc->heartbeat, now, __ATOMIC_RELAXED );
+      int err = fd_verify_tile_service( a->tile, 0 );      /* publish completed batches, in order */
+      if( err ) { a->err = err; fd_vt_diag_push( a, in_backp, backp_cnt ); fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+      fd_vt_diag_push( a, in_backp, backp_cnt );
+      unsigned long s = fd_vt_cnc_query( cnc );
+      if( s != FD_VERIFY_TILE_SIGNAL_RUN ) {
+        if( s != FD_VERIFY_TILE_SIGNAL_HALT ) { a->err = FD_ED25519_ERR_ARG; fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+        break;
+      }
+      cr_avail = a->cr_avail ? a->cr_avail( a->cr_ctx ) : ~0UL;
+      if( in_backp && cr_avail ) in_backp = 0;
+      /* reload with jitter in [lazy/2, lazy) (fd_tempo_async_reload) */
+      rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+      then = now + lazy / 2L + (long)(rng % (unsigned long)(lazy / 2L + 1L));
+    }
+    /* backpressure (fd_frank_verify.c:185-194) */
+    if( !cr_avail ) {
+      if( !in_backp ) { in_backp = 1; backp_cnt++; }
+      __builtin_ia32_pause();
+      now = fd_vt_now();
+      continue;
+    }
+    /* the frag path (the reference's placeholder, :196-203) */
+    void const * frag; unsigned long sz, ctl, tsorig;
+    if( a->in( a->in_ctx, &frag, &sz, &ctl, &tsorig ) > 0 ) {
+      int err = fd_verify_tile_rx( a->tile, frag, sz, ctl, tsorig );
+      if( err ) { a->err = err; fd_vt_diag_push( a, in_backp, backp_cnt ); fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+      if( cr_avail != ~0UL ) cr_avail--;
+    } else {
+      __builtin_ia32_pause();
+    }
+    now = fd_vt_now();
+  }
+  /* HALT: submit the partial batch, publish everything in flight, report,
+     then BOOT (can be booted again) */
+  int err = fd_verify_tile_service( a->tile, 1 );
+  fd_vt_diag_push( a, in_backp, backp_cnt );
+  if( err ) { a->err = err; fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+  fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_BOOT );
+}
+
+static void fd_vt_task_fini( fd_verify_tile_args_t * a ) {
+  fd_verify_tile_delete( a->tile ); a->tile = NULL;
+  fd_ed25519_gpu_delete( a->gpu );  a->gpu  = NULL;
+}
+
+FD_EXPORT fd_verify_tile_task_t fd_verify_tile_task = {
+  "verify",
+  fd_vt_task_init,
+  fd_vt_task_run,
+  fd_vt_task_fini,
+};
+
+FD_EXPORT fd_verify_tile_task_t const * fd_verify_tile_task_get( void ) { return &fd_verify_tile_task; }

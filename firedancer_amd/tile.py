@@ -9,7 +9,7 @@ import numpy as np
 from . import EngineError, _p, last_error, lib
 
 DIAG = ("IN_BACKP", "BACKP_CNT", "HA_FILT_CNT", "HA_FILT_SZ", "SV_FILT_CNT", "SV_FILT_SZ",
-        "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT")
+        "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT", "RING_FULL_CNT")
 
 PUBLISH_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_ulong,
                               ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong)
@@ -90,3 +90,103 @@ class VerifyTile:
             self.close()
         except Exception:
             pass
+
+
+# ---- the tile as a task (fd_verify_tile_task, include/fd_verify_tile.h) ----
+
+SIGNAL_RUN, SIGNAL_BOOT, SIGNAL_FAIL, SIGNAL_HALT = 0, 1, 2, 3
+
+IN_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_ulong),
+                         ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong))
+CR_FN = ctypes.CFUNCTYPE(ctypes.c_ulong, ctypes.c_void_p)
+
+
+class Cnc(ctypes.Structure):
+    _fields_ = [("signal", ctypes.c_ulong), ("heartbeat", ctypes.c_long), ("diag", ctypes.c_ulong * len(DIAG))]
+
+
+class Args(ctypes.Structure):
+    """fd_verify_tile_args_t"""
+    _fields_ = [("device", ctypes.c_int), ("max_sigs", ctypes.c_ulong), ("max_blob", ctypes.c_ulong),
+                ("depth", ctypes.c_int), ("cfg", Cfg), ("cnc", ctypes.POINTER(Cnc)),
+                ("in_fn", ctypes.c_void_p), ("in_ctx", ctypes.c_void_p),
+                ("publish", ctypes.c_void_p), ("pub_ctx", ctypes.c_void_p),
+                ("cr_avail", ctypes.c_void_p), ("cr_ctx", ctypes.c_void_p),
+                ("lazy_ns", ctypes.c_long),
+                ("close_fd_start", ctypes.c_uint), ("allow_syscalls_sz", ctypes.c_ushort),
+                ("allow_syscalls", ctypes.POINTER(ctypes.c_long)),
+                ("gpu", ctypes.c_void_p), ("tile", ctypes.c_void_p), ("err", ctypes.c_int)]
+
+
+class TaskFns(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("init", ctypes.c_void_p), ("run", ctypes.c_void_p), ("fini", ctypes.c_void_p)]
+
+
+class Task:
+    """fd_verify_tile_task driven from Python: frags from a list (the input
+    mcache), publishes collected, optional credit schedule (the fctl).
+    run() blocks until the cnc is signalled HALT (call halt() from
+    another thread) or the task fails."""
+
+    def __init__(self, frags, device=0, max_sigs=4096, max_blob=8 << 20, depth=3, batch_sigs=0,
+                 credits=None, lazy_ns=0):
+        L = lib()
+        L.fd_verify_tile_task_get.restype = ctypes.POINTER(TaskFns)
+        fns = L.fd_verify_tile_task_get().contents
+        self.name = fns.name.decode()
+        V = ctypes.CFUNCTYPE(None, ctypes.POINTER(Args))
+        self._init, self._run, self._fini = V(fns.init), V(fns.run), V(fns.fini)
+        self.frags = [ctypes.create_string_buffer(bytes(f), len(f)) for f in frags]
+        self.sizes = [len(f) for f in frags]
+        self.next = 0
+        self.published = []
+        self.credits = credits
+        self.cnc = Cnc()
+        self.cnc.signal = SIGNAL_BOOT
+        self._in = IN_FN(self._on_in)
+        self._pub = PUBLISH_FN(self._on_publish)
+        self._cr = CR_FN(self._on_cr) if credits is not None else None
+        a = Args()
+        a.device, a.max_sigs, a.max_blob, a.depth = device, max_sigs, max_blob, depth
+        a.cfg = Cfg(batch_sigs, 16, 64)
+        a.cnc = ctypes.pointer(self.cnc)
+        a.in_fn = ctypes.cast(self._in, ctypes.c_void_p)
+        a.publish = ctypes.cast(self._pub, ctypes.c_void_p)
+        a.cr_avail = ctypes.cast(self._cr, ctypes.c_void_p) if self._cr else None
+        a.lazy_ns = lazy_ns
+        self.args = a
+
+    def _on_in(self, ctx, frag, sz, ctl, tsorig):
+        if self.next >= len(self.frags):
+            return 0
+        i = self.next
+        self.next += 1
+        frag[0] = ctypes.cast(self.frags[i], ctypes.c_void_p).value
+        sz[0], ctl[0], tsorig[0] = self.sizes[i], i, 1000 + i
+        return 1
+
+    def _on_publish(self, ctx, sig, frag, sz, ctl, tsorig, tspub):
+        self.published.append((sig, ctypes.string_at(frag, sz), ctl, tsorig))
+
+    def _on_cr(self, ctx):
+        return int(self.credits(self))
+
+    def init(self):
+        self._init(ctypes.byref(self.args))
+        return self.args.err
+
+    def allow_syscalls(self):
+        return [self.args.allow_syscalls[i] for i in range(self.args.allow_syscalls_sz)]
+
+    def run(self):
+        self._run(ctypes.byref(self.args))
+        return self.args.err
+
+    def halt(self):
+        self.cnc.signal = SIGNAL_HALT
+
+    def diag(self) -> dict:
+        return dict(zip(DIAG, list(self.cnc.diag)))
+
+    def fini(self):
+        self._fini(ctypes.byref(self.args))

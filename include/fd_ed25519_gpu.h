@@ -185,6 +185,17 @@ fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * gpu, int groups );
 int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
 
+/* Which quad-DSM form small batches take: the one-wave-per-SIMD form
+   (Ai tables, Bi and op streams in 34 KiB of LDS per wave: the lowest
+   latency for a lone batch) or the two-waves-per-SIMD form (20 KiB: more
+   throughput when batches share the chip).  RING (default): the second
+   while another ring batch is in flight.  Codes are identical. */
+#define FD_ED25519_GPU_QUAD2_NEVER  (0)
+#define FD_ED25519_GPU_QUAD2_RING   (1)
+#define FD_ED25519_GPU_QUAD2_ALWAYS (2)
+int fd_ed25519_gpu_set_quad2( fd_ed25519_gpu_t * gpu, int policy );
+int fd_ed25519_gpu_quad2    ( fd_ed25519_gpu_t const * gpu );
+
 /* Register a host region the ring may DMA from in place
    (hipHostRegister; call before sandboxing, e.g. on the tile's input
    dcache).  A submitted blob lying inside a registered region is copied

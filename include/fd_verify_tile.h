@@ -55,7 +55,11 @@ extern "C" {
 #define FD_VERIFY_TILE_DIAG_BAD_CNT     (8UL)  /* malformed frags dropped    */
 #define FD_VERIFY_TILE_DIAG_SIG_CNT     (9UL)  /* signatures sent to the GPU */
 #define FD_VERIFY_TILE_DIAG_BATCH_CNT   (10UL) /* GPU batches submitted      */
-#define FD_VERIFY_TILE_DIAG_CNT         (11UL)
+#define FD_VERIFY_TILE_DIAG_RING_FULL_CNT (11UL) /* waits for a free ring slot */
+#define FD_VERIFY_TILE_DIAG_CNT         (12UL)
+/* IN_BACKP / BACKP_CNT are the flow-control backpressure diagnostics of
+   the reference (fd_frank_verify.c:185-194): maintained by the task's run
+   loop (fd_verify_tile_task below); the bare tile object reports 0. */
 
 typedef struct {
   unsigned long batch_sigs;      /* signatures per GPU batch (<= engine max_sigs); 0 -> engine max */
@@ -112,6 +116,70 @@ int fd_verify_tile_service( fd_verify_tile_t * tile, int flush );
 
 /* Snapshot of the diagnostic counters (FD_VERIFY_TILE_DIAG_CNT slots). */
 void fd_verify_tile_diag( fd_verify_tile_t const * tile, unsigned long * diag );
+
+/* ---- The tile as a task (fd_frank_task_t shape, fd_frank.h:29-45) -----
+
+   fd_verify_tile_task.init creates all device state (engine: HIP
+   runtime, device memory, pinned ring, streams; the tile) before the
+   caller sandboxes the process, and reports the extended seccomp
+   allowlist and close_fd_start; .run is the reference tile's run loop
+   (fd_frank_verify.c:139-204) with its placeholder filled in -- it never
+   returns until the cnc is signalled HALT (drains, publishes, BOOT) or it
+   fails (FAIL); .fini frees the device state.
+
+   Tango itself is out of scope: the input mcache/dcache, the output
+   fctl and the cnc are passed as a frag source callback, a credit
+   callback and a cnc-shaped struct. */
+
+/* cnc signals (src/tango/cnc/fd_cnc.h:105-108) */
+#define FD_VERIFY_TILE_SIGNAL_RUN  (0UL)
+#define FD_VERIFY_TILE_SIGNAL_BOOT (1UL)
+#define FD_VERIFY_TILE_SIGNAL_FAIL (2UL)
+#define FD_VERIFY_TILE_SIGNAL_HALT (3UL)
+
+typedef struct {
+  unsigned long signal;                            /* BOOT before run; run sets RUN; a cnc thread sets HALT */
+  long          heartbeat;                         /* CLOCK_MONOTONIC ns of the last housekeeping */
+  unsigned long diag[ FD_VERIFY_TILE_DIAG_CNT ];   /* the cnc app region */
+} fd_verify_tile_cnc_t;
+
+/* next input frag: 1 and *frag/sz/ctl/tsorig set, or 0 if none yet (the
+   reference tile's mcache poll) */
+typedef int (*fd_verify_tile_in_fn)( void * ctx, void const ** frag, unsigned long * sz,
+                                     unsigned long * ctl, unsigned long * tsorig );
+/* downstream credits available (fd_fctl_tx_cr_update); 0 = backpressured */
+typedef unsigned long (*fd_verify_tile_cr_fn)( void * ctx );
+
+typedef struct {
+  /* set by the caller (the reference reads these from its pod) */
+  int                        device;
+  unsigned long              max_sigs, max_blob;    /* engine batch capacity */
+  int                        depth;                 /* ring slots, 0 -> 3 */
+  fd_verify_tile_cfg_t       cfg;
+  fd_verify_tile_cnc_t *     cnc;
+  fd_verify_tile_in_fn       in;       void * in_ctx;
+  fd_verify_tile_publish_fn  publish;  void * pub_ctx;
+  fd_verify_tile_cr_fn       cr_avail; void * cr_ctx;   /* NULL: never backpressured */
+  long                       lazy_ns;               /* housekeeping interval, <= 0: 100 us */
+  /* set by init (fd_frank_args_t fields) */
+  unsigned int               close_fd_start;
+  unsigned short             allow_syscalls_sz;
+  long const *               allow_syscalls;
+  /* state */
+  fd_ed25519_gpu_t *         gpu;
+  fd_verify_tile_t *         tile;
+  int                        err;                   /* 0, or why init / run failed */
+} fd_verify_tile_args_t;
+
+typedef struct {
+  char const * name;
+  void (*init)( fd_verify_tile_args_t * args );
+  void (*run )( fd_verify_tile_args_t * args );
+  void (*fini)( fd_verify_tile_args_t * args );
+} fd_verify_tile_task_t;
+
+extern fd_verify_tile_task_t fd_verify_tile_task;
+fd_verify_tile_task_t const * fd_verify_tile_task_get( void );
 
 /* HA dedup cache on its own (tests): a sliding window of the last depth
    distinct tags, FD_TCACHE_INSERT semantics (src/tango/tcache/

@@ -1,0 +1,92 @@
+/* fake_engine.cpp -- TEST INFRASTRUCTURE ONLY (tests/sanitize/): a CPU
+   stand-in for the subset of the engine ABI (include/fd_ed25519_gpu.h)
+   the verify tile uses (new_ex/delete/max_sigs/max_blob/depth/stage/
+   unstage/submit/poll), so the tile's host logic runs under ASan/UBSan
+   and libFuzzer without a GPU.  Codes come from the CPU restatement
+   (oracle/fd_ed25519_oracle.c, itself pinned to the reference build);
+   descriptors outside the blob get FD_ED25519_ERR_ARG exactly as the
+   device reports them.  Ring semantics follow fd_ed25519_gpu_host.cpp:
+   a staged slot's buffers are the caller's zero-copy blob; a poll without
+   block reports "not yet" on every other ticket to exercise that path. */
+#include <stdlib.h>
+#include <string.h>
+#include "fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_desc.h"
+
+extern "C" int oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
+
+#define FAKE_DEPTH_MAX 8
+struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket; int staged, polls; };
+struct fd_ed25519_gpu {
+  unsigned long max_sigs, max_blob, next; int depth;
+  fake_slot slot[ FAKE_DEPTH_MAX ];
+};
+
+extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long max_sigs, unsigned long max_blob, int depth ) {
+  (void)device;
+  if( !max_sigs || depth < 1 || depth > FAKE_DEPTH_MAX ) return NULL;
+  fd_ed25519_gpu_t * g = (fd_ed25519_gpu_t *)calloc( 1, sizeof(*g) );
+  g->max_sigs = max_sigs; g->max_blob = max_blob; g->depth = depth; g->next = 1;
+  for( int s=0; s<depth; s++ ) {
+    g->slot[s].blob = (uint8_t *)malloc( max_blob + 64UL );      /* exactly the engine's pinned blob + pad */
+    g->slot[s].desc = (fd_ed25519_gpu_desc_t *)malloc( max_sigs * sizeof(fd_ed25519_gpu_desc_t) );
+    g->slot[s].out  = (int *)malloc( max_sigs * sizeof(int) );
+  }
+  return g;
+}
+extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_sigs, unsigned long max_blob ) {
+  return fd_ed25519_gpu_new_ex( device, max_sigs, max_blob, 3 );
+}
+extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
+  if( !g ) return;
+  for( int s=0; s<g->depth; s++ ) { free( g->slot[s].blob ); free( g->slot[s].desc ); free( g->slot[s].out ); }
+  free( g );
+}
+extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g->max_sigs; }
+extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g->max_blob; }
+extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g->depth; }
+
+extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
+  for( int s=0; s<g->depth; s++ ) {
+    fake_slot * sl = &g->slot[s];
+    if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->blob; *desc = sl->desc; return 0; }
+  }
+  return FD_ED25519_ERR_ARG;
+}
+extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].blob == blob ) g->slot[s].staged = 0;
+}
+
+extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+  fake_slot * sl = NULL;
+  for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && g->slot[s].blob == blob ) sl = &g->slot[s];
+  for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) sl = &g->slot[s];
+  if( !sl ) return FD_ED25519_ERR_ARG;
+  if( sl->blob != blob ) memcpy( sl->blob, blob, blob_sz );
+  if( sl->desc != desc ) memcpy( sl->desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_ed25519_gpu_desc_t const * d = &sl->desc[i];
+    sl->out[i] = fd_ed25519_desc_ok( d, blob_sz )
+               ? oracle_verify( sl->blob + d->msg_off, d->msg_sz, sl->blob + d->sig_off, sl->blob + d->pub_off )
+               : FD_ED25519_ERR_ARG;
+  }
+  sl->n = n; sl->staged = 0; sl->polls = 0;
+  sl->ticket = g->next++;
+  *ticket = sl->ticket;
+  return 0;
+}
+
+extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
+  if( !g || !ticket ) return FD_ED25519_ERR_ARG;
+  for( int s=0; s<g->depth; s++ ) {
+    fake_slot * sl = &g->slot[s];
+    if( sl->ticket != ticket ) continue;
+    if( !block && (ticket & 1UL) && !sl->polls++ ) return 0;   /* "still in flight" once */
+    if( out ) memcpy( out, sl->out, sl->n * sizeof(int) );
+    sl->ticket = 0;
+    return 1;
+  }
+  return FD_ED25519_ERR_ARG;
+}

@@ -282,3 +282,33 @@ def test_quad_q2_vectors(engine):
     assert len(b) <= engine.dsm_quad_max
     got = engine.verify_packed(b.blob, b.desc)
     assert got.tolist() == [v["expected"] for v in vs]
+
+
+@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
+def test_quad2_golden_corpora(name):
+    """the two-waves-per-SIMD quad DSM (fd_k_dsm_quad2: unpadded Ai in LDS,
+    op bytes and Bi from global memory) gives the reference's codes"""
+    e = fa.Engine(0, 1 << 14, 1 << 24, depth=1)
+    try:
+        e.quad2 = fa.QUAD2_ALWAYS
+        b, exp = load_corpus(name)
+        got = e.verify_packed(b.blob, b.desc)
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("n", [1, 15, 17, 4096 + 77, 30000])
+def test_quad2_equals_quad(engine, n):
+    base, _ = load_corpus("adversarial")
+    b = base.tile(int(np.ceil(n / len(base))))
+    b.desc = b.desc[:n]
+    e = fa.Engine(0, 1 << 15, 1 << 24, depth=1)
+    try:
+        e.quad2 = fa.QUAD2_ALWAYS
+        q2 = e.verify_packed(b.blob, b.desc)
+    finally:
+        e.close()
+    q = engine.verify_packed(b.blob, b.desc)
+    assert (q == q2).all(), np.nonzero(q != q2)[0][:10]

@@ -1,0 +1,94 @@
+"""Sanitizer and fuzz coverage of the host code that handles untrusted
+input (CPU only; tests/sanitize/Makefile), as the reference builds its C
+with ASan/UBSan and fuzzes its parser (config/with-asan.mk,
+config/linux_clang_x86_64_fuzz_asan.mk, src/ballet/txn/fuzz_txn_parse.c):
+
+  - the product txn parser's mutation sweep (test_mutate's input set)
+    under ASan/UBSan, its output stream hashed against the REFERENCE
+    parser's golden digest;
+  - the verify tile + tcache + parser on a CPU fake engine under
+    ASan/UBSan: a stream whose publish set must equal the reference's
+    per-frag expectation, then corrupted streams checked for the tile's
+    accounting invariants;
+  - libFuzzer runs of fd_txn_parse, the tile's frag path and the ring
+    feeders' descriptor span / rebase / chunk logic."""
+import hashlib
+import json
+import os
+import struct
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+SAN = os.path.join(ROOT, "tests", "sanitize")
+BUILD = os.path.join(SAN, "build")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+
+@pytest.fixture(scope="module")
+def built():
+    r = subprocess.run(["make", "-j8", "-C", SAN], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return BUILD
+
+
+def test_txn_parser_mutation_sweep_asan(built):
+    gold = json.load(open(os.path.join(GOLDEN, "txn_parse_golden.json")))
+    for k, name in enumerate(("transaction1.bin", "transaction2.bin", "transaction3.bin")):
+        p = os.path.join(GOLDEN, name)
+        r = subprocess.run([os.path.join(built, "san_txn"), p], capture_output=True, env=ENV)
+        assert r.returncode == 0, r.stderr[-3000:].decode(errors="replace")
+        out = r.stdout
+        # the stream is (truncation fp, 255 x (fp [+ descriptor])) per byte, then the counters
+        ctr_sz = 8 + 8 + 8 * 32
+        body, ctr = out[:-ctr_sz], out[-ctr_sz:]
+        h = hashlib.sha256(body).hexdigest()
+        assert h == gold["sweep"][k]["sha256"], name
+        succ, fail = struct.unpack_from("<QQ", ctr)
+        assert (succ, fail) == (gold["sweep"][k]["success_cnt"], gold["sweep"][k]["failure_cnt"])
+        assert list(struct.unpack_from("<32Q", ctr, 16)) == gold["sweep"][k]["failure_ring"]
+
+
+def test_verify_tile_asan_vs_reference(built, ref, tmp_path):
+    from test_verify_tile import expected_for, make_stream
+    frags = make_stream(1500, 91, ref)
+    exp_pub, exp, _ = expected_for(frags, ref)
+    p = tmp_path / "frags.bin"
+    with open(p, "wb") as f:
+        f.write(struct.pack("<I", len(frags)))
+        for fr in frags:
+            f.write(struct.pack("<I", len(fr)) + fr)
+    r = subprocess.run([os.path.join(built, "san_tile"), str(p), "8"], capture_output=True, text=True, env=ENV, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines()]
+    first = lines[0]
+    h = 1469598103934665603
+    for tag, fr in exp_pub:
+        for byte in fr:
+            h = ((h ^ byte) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+        for byte in struct.pack("<QQ", tag, len(fr)):
+            h = ((h ^ byte) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    assert first["rc"] == 0 and first["pub_cnt"] == len(exp_pub) and int(first["pub_hash"], 16) == h
+    from firedancer_amd.tile import DIAG
+    d = dict(zip(DIAG, first["diag"]))
+    for k, v in exp.items():
+        assert d[k] == v, k
+    assert len(lines) == 9 and all(x["rc"] == 0 for x in lines)
+    assert sum(x.get("bad", 0) for x in lines[1:]) > 0
+
+
+@pytest.mark.parametrize("target,secs", [("fuzz_txn_parse", 20), ("fuzz_verify_tile", 25), ("fuzz_desc", 15)])
+def test_libfuzzer(built, tmp_path, target, secs):
+    corpus_dir = tmp_path / "corpus"
+    corpus_dir.mkdir()
+    if target == "fuzz_txn_parse":
+        for name in ("transaction1.bin", "transaction2.bin", "transaction3.bin"):
+            (corpus_dir / name).write_bytes(open(os.path.join(GOLDEN, name), "rb").read())
+    env = dict(ENV)
+    r = subprocess.run([os.path.join(built, target), f"-max_total_time={secs}", "-rss_limit_mb=4096",
+                        "-print_final_stats=1", str(corpus_dir)],
+                       capture_output=True, text=True, env=env, timeout=secs + 120, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "Done" in r.stderr and "ERROR" not in r.stderr

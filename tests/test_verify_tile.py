@@ -76,11 +76,10 @@ def make_stream(n_sigs, seed, ref):
     return frags
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("batch_sigs", [256, 4096])
-def test_tile_stream_vs_reference(engine, ref, batch_sigs):
-    frags = make_stream(6000, 21 + batch_sigs, ref)
-    # expected, frag by frag, with the reference's tcache and verify
+def expected_for(frags, ref):
+    """(published (tag, frag) in order, diag counters) frag by frag with the
+    reference's tcache and fd_ed25519_verify
+    (fd_frank_verify_synth_load.c:360-410)"""
     r = _ref_tc(ref, 16, 64)
     exp_pub, exp = [], dict(HA_FILT_CNT=0, HA_FILT_SZ=0, SV_FILT_CNT=0, SV_FILT_SZ=0, BAD_CNT=0)
     blob, descs, owners, cand = [], [], [], []
@@ -113,6 +112,14 @@ def test_tile_stream_vs_reference(engine, ref, batch_sigs):
         else:
             exp["SV_FILT_CNT"] += 1
             exp["SV_FILT_SZ"] += len(f)
+    return exp_pub, exp, len(codes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch_sigs", [256, 4096])
+def test_tile_stream_vs_reference(engine, ref, batch_sigs):
+    frags = make_stream(6000, 21 + batch_sigs, ref)
+    exp_pub, exp, nsig = expected_for(frags, ref)
     assert 0 < exp["SV_FILT_CNT"] and 0 < exp["HA_FILT_CNT"] and 0 < exp["BAD_CNT"]
 
     tile = VerifyTile(engine, batch_sigs=batch_sigs)
@@ -129,7 +136,7 @@ def test_tile_stream_vs_reference(engine, ref, batch_sigs):
     d = tile.diag()
     for k, v in exp.items():
         assert d[k] == v, k
-    assert d["PUB_CNT"] == len(exp_pub) and d["SIG_CNT"] == len(codes)
+    assert d["PUB_CNT"] == len(exp_pub) and d["SIG_CNT"] == nsig
     tile.close()
 
 

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--groups", default="1,2,3,4")
     ap.add_argument("--windows", default="1")
     ap.add_argument("--no-register", action="store_true")
+    ap.add_argument("--quad2", default="1", help="comma list of quad2 policies (0 never, 1 ring, 2 always)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime, firedancer_amd._share_hip_runtime)
     import bench
@@ -32,8 +33,9 @@ def main():
             if g > d:
                 continue
             for w in [int(x) for x in a.windows.split(",")]:
-                r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w * d, register=not a.no_register)
-                print(json.dumps(r), flush=True)
+                for q in [int(x) for x in a.quad2.split(",")]:
+                    r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w * d, register=not a.no_register, quad2=q)
+                    print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
