@@ -228,7 +228,9 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   g->timeout_ns = FD_WAIT_TIMEOUT_NS_DEFAULT;
-  g->quad2 = FD_ED25519_GPU_QUAD2_RING;
+  /* measured slower on the ring at every depth (profiles/r02_ring_sweep_quad2.jsonl):
+     one quad wave already keeps its SIMD busy */
+  g->quad2 = FD_ED25519_GPU_QUAD2_NEVER;
   { char const * q2 = getenv( "FD_ED25519_GPU_QUAD2" ); if( q2 ) g->quad2 = atoi( q2 ); }   /* experiments */
   /* a slot's pinned and device blob buffers also hold the batch's
      descriptors, 16-aligned after the padded blob, so a batch is ONE H2D

@@ -28,8 +28,8 @@
    runtime issues after init on the tile's hot path: ioctl (KFD/DRM event
    waits and queue doorbells), mmap / munmap / mprotect / madvise (runtime
    memory-pool growth), sched_yield (runtime spin-waits),
-   clock_nanosleep (glibc's nanosleep) and get_mempolicy (the runtime's
-   NUMA queries on the copy path).  Checked on an MI355X by
+   clock_nanosleep (glibc's nanosleep), get_mempolicy and mbind (NUMA
+   placement when the runtime grows a memory pool).  Checked on an MI355X by
    tests/test_verify_tile_task.py::test_task_under_seccomp (a seccomp
    filter that allows exactly this list around the whole run loop). */
 static long const fd_vt_allow_syscalls[] = {
@@ -44,7 +44,8 @@ static long const fd_vt_allow_syscalls[] = {
   __NR_madvise,
   __NR_sched_yield,     /* HIP spin-waits */
   __NR_clock_nanosleep, /* glibc nanosleep */
-  __NR_get_mempolicy,   /* HIP: NUMA placement queries on the copy path */
+  __NR_get_mempolicy,   /* HIP: NUMA placement of runtime pool growth */
+  __NR_mbind,
 };
 
 static long fd_vt_now( void ) {

@@ -188,8 +188,10 @@ int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
 /* Which quad-DSM form small batches take: the one-wave-per-SIMD form
    (Ai tables, Bi and op streams in 34 KiB of LDS per wave: the lowest
    latency for a lone batch) or the two-waves-per-SIMD form (20 KiB: more
-   throughput when batches share the chip).  RING (default): the second
-   while another ring batch is in flight.  Codes are identical. */
+   throughput only where a lone wave leaves its SIMD idle).  NEVER is the
+   default: on MI355X one quad wave already keeps its SIMD busy, and the
+   second form measured slower for ring streams at every depth; RING
+   takes it while another ring batch is in flight.  Codes are identical. */
 #define FD_ED25519_GPU_QUAD2_NEVER  (0)
 #define FD_ED25519_GPU_QUAD2_RING   (1)
 #define FD_ED25519_GPU_QUAD2_ALWAYS (2)
