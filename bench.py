@@ -100,6 +100,7 @@ def parse():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
     ap.add_argument("--ring-depth", type=int, default=6, help="ring slots of the C2 streaming leg")
+    ap.add_argument("--dry-cpu", action="store_true", help="rehearse the multi-rank plumbing on the CPU (tests only)")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
@@ -177,11 +178,100 @@ def _cpu_model():
     return "unknown"
 
 
+def timed_region(step, steps, warmup, dist, red_dev, sync):
+    """W untimed warmup steps, then exactly K steps bracketed by a barrier +
+    device sync on both sides; returns the MAX over ranks of the wall time."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def all_ranks_ok(ok, dist, red_dev):
+    if not dist:
+        return ok
+    import torch
+    okt = torch.tensor([1 if ok else 0], device=red_dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    return bool(okt.item())
+
+
+def dry_cpu(a, rank, world):
+    """Rehearsal of the N-rank plumbing on the CPU (tests/test_bench_dist.py):
+    torch.distributed.run launch, gloo barrier, max-over-ranks timing and
+    the whole-job aggregate, with a fixed host step standing in for the
+    GPU launch.  Never a measurement: data says so."""
+    import torch.distributed as torch_dist
+    dist = None
+    if world > 1:
+        torch_dist.init_process_group("gloo")
+        dist = torch_dist
+    n_step = a.step_batches * BATCH_SIGS
+    x = np.arange(1 << 16, dtype=np.uint64)
+
+    def step():
+        np.bitwise_xor.reduce(x * np.uint64(2654435761 + rank))
+
+    elapsed = timed_region(step, a.steps, a.warmup, dist, "cpu", lambda: None)
+    ok = all_ranks_ok(True, dist, "cpu")
+    res = result_line(a, world, n_step, elapsed, ok, None)
+    res["data"] = "dry-cpu rehearsal of the multi-rank plumbing (no GPU, no verification): not a measurement"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def result_line(a, world, n_step, elapsed, ok, base):
+    total = n_step * a.steps * world
+    return {
+        "metric": "Ed25519 verifies/sec at 1/2/4/8 MI355X; p99 latency per 4096-sig batch",
+        "value": total / elapsed,
+        "unit": "verifies/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: 4096-signature batches of 1232-byte Solana legacy txns, 1-2 sigs/txn (p=0.7/0.3), all valid",
+            "batch_sigs": BATCH_SIGS,
+            "batches_per_step": a.step_batches,
+            "sigs_per_step_per_gpu": n_step,
+            "unique_sigs_per_gpu": len(base) if base is not None else None,
+            "msg_sz": sorted(set(int(x) for x in np.unique(base.desc["msg_sz"]))) if base is not None else None,
+            "parallelism": f"replicas x{world} (independent per-GPU shards, no collective)",
+        },
+        "all_accepted": ok,
+    }
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_cpu:
+        return dry_cpu(a, rank, world)
     import torch
     dist = None
     # rehearsal only (FD_BENCH_SHARE_GPU=1): more ranks than GPUs share them,
@@ -221,55 +311,14 @@ def main():
     def step():
         eng.verify_dev(n_step, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), stream)
 
-    for _ in range(a.warmup):
-        step()
+    # the first warmup step's codes are checked (all valid: all accepted)
+    step()
     torch.cuda.synchronize()
     ok = bool((d_out == 0).all().item())
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], device=red_dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-
-    total = n_step * a.steps * world
-    value = total / elapsed
-    res = {
-        "metric": "Ed25519 verifies/sec at 1/2/4/8 MI355X; p99 latency per 4096-sig batch",
-        "value": value,
-        "unit": "verifies/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": elapsed / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic",
-        "config": {
-            "workload": "C2: 4096-signature batches of 1232-byte Solana legacy txns, 1-2 sigs/txn (p=0.7/0.3), all valid",
-            "batch_sigs": BATCH_SIGS,
-            "batches_per_step": a.step_batches,
-            "sigs_per_step_per_gpu": n_step,
-            "unique_sigs_per_gpu": len(base),
-            "msg_sz": sorted(set(int(x) for x in np.unique(base.desc["msg_sz"]))),
-            "parallelism": f"replicas x{world} (independent per-GPU shards, no collective)",
-        },
-        "all_accepted": ok,
-    }
+    elapsed = timed_region(step, a.steps, max(a.warmup - 1, 0), dist, red_dev, torch.cuda.synchronize)
+    ok = all_ranks_ok(ok, dist, red_dev)
+    res = result_line(a, world, n_step, elapsed, ok, base)
+    value = res["value"]
 
     if rank == 0 and world == 1:
         # per-kernel durations over the same launches, on the launch stream

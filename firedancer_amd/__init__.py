@@ -187,6 +187,8 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_feeder_new.restype = vp
         L.fd_ed25519_gpu_feeder_delete.argtypes = [vp]
         L.fd_ed25519_gpu_feeder_delete.restype = None
+        L.fd_ed25519_gpu_device_numa_node.argtypes = [ip]
+        L.fd_ed25519_gpu_device_numa_node.restype = ip
         L.fd_ed25519_gpu_feeder_numa_node.argtypes = [vp]
         L.fd_ed25519_gpu_feeder_numa_node.restype = ip
         L.fd_ed25519_gpu_feeder_push.argtypes = [vp, vp]
@@ -545,6 +547,18 @@ def verify_batch_single_msg(msg: bytes, sigs: np.ndarray, pubs: np.ndarray) -> t
 
 def device_count() -> int:
     return lib().fd_ed25519_gpu_device_cnt()
+
+
+def numa_cpus(device: int) -> list:
+    """CPUs of the device's NUMA node this process may use ([] if unknown)."""
+    node = lib().fd_ed25519_gpu_device_numa_node(device)
+    if node < 0:
+        return []
+    cpus = set()
+    for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return sorted(cpus & os.sched_getaffinity(0))
 
 
 def sign_batch(seeds: np.ndarray, blob: np.ndarray, msg_off: np.ndarray, msg_sz: np.ndarray, nthreads: int = 8):

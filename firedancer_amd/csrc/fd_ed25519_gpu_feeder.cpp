@@ -194,6 +194,11 @@ FD_EXPORT fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_feeder_new( fd_ed25519_gpu_t 
   return f;
 }
 
+FD_EXPORT int fd_ed25519_gpu_device_numa_node( int device ) {
+  cpu_set_t set; CPU_ZERO( &set );
+  return fd_feeder_numa_cpus( device, &set );
+}
+
 FD_EXPORT int fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * f ) { return f ? f->numa_node : -1; }
 
 FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {

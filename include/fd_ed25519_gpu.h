@@ -332,6 +332,9 @@ typedef struct fd_ed25519_gpu_feeder fd_ed25519_gpu_feeder_t;
 fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_feeder_new( fd_ed25519_gpu_t * gpu, int pin_numa );
 /* Drains: every pushed job completes before the thread exits. */
 void fd_ed25519_gpu_feeder_delete   ( fd_ed25519_gpu_feeder_t * feeder );
+/* NUMA node of a device's PCI function whose CPUs this process may use
+   (sysfs numa_node and cpulist vs the affinity mask), -1 if none. */
+int  fd_ed25519_gpu_device_numa_node( int device );
 /* NUMA node the feeder thread is pinned to, -1 if none. */
 int  fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * feeder );
 /* Queue a job (n <= the engine's max_sigs; the referenced span must fit

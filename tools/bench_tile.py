@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
-"""C5 (BASELINE.json configs[4]) on one GPU: a sustained stream of
-QUIC-format frags (Solana-MTU txns, 1..12 signatures, uniform) through
-the verify tile (HA dedup -> pinned staging -> GPU batches -> in-order
-publish), host-fed from one thread, PCIe included.  Prints one JSON
-line: sustained verifies/s and txns/s over --seconds of streaming.
+"""C5 (BASELINE.json configs[4]): a sustained stream of QUIC-format frags
+(Solana-MTU txns, 1..12 signatures, uniform) through verify tiles (HA
+dedup -> pinned staging -> GPU batches -> in-order publish), each tile
+host-fed from its own thread pinned to its GPU's NUMA node, PCIe
+included.  Prints one JSON line: sustained verifies/s and txns/s over
+--seconds of streaming.
 
-Multi-GPU: run one process per GPU (python -m torch.distributed.run
---nproc-per-node N tools/bench_tile.py); each rank is an independent tile
-on its own device and shard, rank 0 prints the sum (replicas, no
-collective on the data path)."""
+Multi-GPU, one process: --gpus N runs --tiles tiles on each of devices
+0..N-1 (tile k on device k mod N), every tile an independent replica on
+its own engine, ring and frag stream (no collective on the data path).
+Multi-GPU, one process per GPU: python -m torch.distributed.run
+--nproc-per-node N tools/bench_tile.py; rank 0 prints the sum.
+FD_BENCH_SHARE_GPU=1 lets --gpus exceed the visible devices (rehearsal
+on one GPU)."""
 import argparse
 import json
 import os
@@ -27,6 +31,7 @@ def main():
     ap.add_argument("--depth", type=int, default=4, help="engine ring slots")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--tiles", type=int, default=1, help="verify tiles per GPU (one host thread + engine each)")
+    ap.add_argument("--gpus", type=int, default=1, help="devices driven from this process, one tile set each")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -49,7 +54,11 @@ def main():
     off = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
 
     import threading
-    engs = [fa.Engine(local, max_sigs=a.batch, max_blob=a.batch * 1400, depth=a.depth) for _ in range(a.tiles)]
+    ndev = fa.device_count()
+    if a.gpus > ndev and os.environ.get("FD_BENCH_SHARE_GPU") != "1":
+        raise SystemExit(f"--gpus {a.gpus} but {ndev} gfx950 devices visible")
+    devs = [local if world > 1 else (k % a.gpus) % max(ndev, 1) for k in range(a.tiles * a.gpus)]
+    engs = [fa.Engine(d, max_sigs=a.batch, max_blob=a.batch * 1400, depth=a.depth) for d in devs]
     tiles = [VerifyTile(e, batch_sigs=a.batch, collect=False) for e in engs]
     for tile in tiles:
         tile.rx_burst(base, off, sz)            # warm-up pass
@@ -57,16 +66,20 @@ def main():
     d0s = [tile.diag() for tile in tiles]
     if dist:
         dist.barrier()
-    passes = [0] * a.tiles
+    passes = [0] * len(tiles)
+    cpus = {d: fa.numa_cpus(d) for d in set(devs)}
     t0 = time.perf_counter()
 
     def feed(k):
+        # the feeding thread on its GPU's NUMA node
+        if cpus[devs[k]]:
+            os.sched_setaffinity(0, cpus[devs[k]])
         # ctypes drops the GIL inside rx_burst: the tiles' host feeds run in parallel
         while time.perf_counter() - t0 < a.seconds:
             tiles[k].rx_burst(base, off, sz)
             passes[k] += 1
         tiles[k].service(flush=True)
-    th = [threading.Thread(target=feed, args=(k,)) for k in range(a.tiles)]
+    th = [threading.Thread(target=feed, args=(k,)) for k in range(len(tiles))]
     for t in th:
         t.start()
     for t in th:
@@ -93,7 +106,9 @@ def main():
         tot = np.array([t[0].item(), t[1].item(), m.item()])
     if rank == 0:
         print(json.dumps({"metric": "sustained verify-tile stream (C5)", "value": tot[0] / tot[2],
-                          "unit": "verifies/s", "txns_per_s": tot[1] / tot[2], "n_gpus": world,
+                          "unit": "verifies/s", "txns_per_s": tot[1] / tot[2],
+                          "n_gpus": world if world > 1 else a.gpus, "devices": sorted(set(devs)),
+                          "numa_nodes": {d: fa.lib().fd_ed25519_gpu_device_numa_node(d) for d in sorted(set(devs))},
                           "seconds": tot[2], "batch_sigs": a.batch, "depth": a.depth, "tiles_per_gpu": a.tiles,
                           "frags_per_pass": len(frags), "sigs_per_pass": a.sigs,
                           "sig_dist": "uniform 1..12 per txn, 1232-byte txns", "pcie_inclusive": True,
