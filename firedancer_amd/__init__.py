@@ -81,8 +81,14 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_verify_packed.restype = ip
         L.fd_ed25519_gpu_verify_dev.argtypes = [vp, ul, vp, ul, vp, vp, vp]
         L.fd_ed25519_gpu_verify_dev.restype = ip
+        L.fd_ed25519_gpu_verify_dev_ex.argtypes = [vp, ul, vp, ul, vp, vp, vp, ip]
+        L.fd_ed25519_gpu_verify_dev_ex.restype = ip
         L.fd_ed25519_gpu_verify_dev_timed.argtypes = [vp, ul, vp, ul, vp, vp, vp, vp]
         L.fd_ed25519_gpu_verify_dev_timed.restype = ip
+        L.fd_ed25519_gpu_dev_stats_begin.argtypes = [vp]
+        L.fd_ed25519_gpu_dev_stats_begin.restype = ip
+        L.fd_ed25519_gpu_dev_stats_end.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fd_ed25519_gpu_dev_stats_end.restype = ip
         L.fd_ed25519_gpu_kernel_cnt.argtypes = []
         L.fd_ed25519_gpu_kernel_cnt.restype = ip
         L.fd_ed25519_public_batch.argtypes = [ul, vp, vp, ip]
@@ -262,10 +268,14 @@ class Engine:
             raise EngineError(f"verify_packed: {strerror(err)}: {last_error()}")
         return out
 
-    def verify_dev(self, n: int, d_blob: int, blob_sz: int, d_desc: int, d_out: int, stream: int = 0) -> None:
+    def verify_dev(self, n: int, d_blob: int, blob_sz: int, d_desc: int, d_out: int, stream: int = 0,
+                   inputs_ready: bool = False) -> None:
         """Device-resident batch (raw device pointers, e.g. torch tensor .data_ptr());
-        blob_sz = payload bytes at d_blob (descriptors are bounds-checked against it)."""
-        err = lib().fd_ed25519_gpu_verify_dev(self._h, n, d_blob, blob_sz, d_desc, d_out, stream or None)
+        blob_sz = payload bytes at d_blob (descriptors are bounds-checked against it).
+        inputs_ready: the inputs are already complete on the device (no ordering
+        after work queued on `stream`), so successive launches overlap."""
+        err = lib().fd_ed25519_gpu_verify_dev_ex(self._h, n, d_blob, blob_sz, d_desc, d_out, stream or None,
+                                                 1 if inputs_ready else 0)
         if err:
             raise EngineError(f"verify_dev: {strerror(err)}: {last_error()}")
 
@@ -278,6 +288,20 @@ class Engine:
         if err:
             raise EngineError(f"verify_dev_timed: {strerror(err)}: {last_error()}")
         return ms
+
+    def dev_stats_begin(self) -> None:
+        """start timing each kernel of the following pipelined verify_dev launches"""
+        if lib().fd_ed25519_gpu_dev_stats_begin(self._h):
+            raise EngineError("dev_stats_begin")
+
+    def dev_stats_end(self):
+        """-> (per-kernel mean ms over the launches since begin, in KERNELS order; launches)"""
+        ms = np.zeros(lib().fd_ed25519_gpu_kernel_cnt(), np.float32)
+        cnt = ctypes.c_ulong(0)
+        err = lib().fd_ed25519_gpu_dev_stats_end(self._h, _p(ms), ctypes.byref(cnt))
+        if err:
+            raise EngineError(f"dev_stats_end: {strerror(err)}: {last_error()}")
+        return (ms / max(cnt.value, 1)).astype(np.float64), cnt.value
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
         """Queue a batch on the pinned ring; returns its ticket."""

@@ -29,6 +29,7 @@
 #define FD_CU_GROUPS         4   /* max default CU groups for small ring batches (1: none) */
 #endif
 #define FD_REG_MAX           16  /* registered host regions per engine */
+#define FD_DEV_STATS_MAX     64  /* pipelined launches timed per stats window */
 #define FD_BLOB_PAD  64UL
 
 static thread_local char fd_gpu_err[256];
@@ -143,13 +144,22 @@ struct fd_ed25519_gpu {
   struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none) */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
-  /* device-resident path (verify_dev / _timed): its own HBM working set,
-     so it never shares scratch with a ring batch; dev_done orders
-     successive device-resident launches on whatever streams they come */
-  fd_ed25519_gpu_work_t dev_work;
-  void *        d_dev_work_base;
-  hipEvent_t    dev_done;
+  /* device-resident path (verify_dev / _timed): its own HBM working sets,
+     so it never shares scratch with a ring batch */
+  /* two working sets, used alternately by successive device-resident
+     launches: launch k's front end (prep, decomp, Ai tables) runs on
+     dev_sf while launch k-1's DSM runs on dev_sb, so it fills the SIMDs
+     the DSM's last round of waves leaves idle (fd_dev_launch) */
+  fd_ed25519_gpu_work_t dev_work[2];
+  void *        d_dev_work_base[2];
+  hipStream_t   dev_sf, dev_sb;
+  hipEvent_t    dev_in[2], dev_front[2], dev_back[2];   /* dev_back[b]: working set b free */
+  unsigned long dev_seq;
   std::mutex    dev_lock;
+  /* per-kernel HIP events of pipelined launches (fd_ed25519_gpu_dev_stats_*) */
+  int           dev_stats_on;
+  unsigned long dev_stats_cnt;
+  hipEvent_t    dev_ev[FD_DEV_STATS_MAX][FD_ED25519_GPU_KERNEL_CNT+1];
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
 };
@@ -274,10 +284,25 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     if( ev ) groups = atoi( ev );
     fd_cu_groups_make( g, groups );
   }
-  HIPCHK( hipMalloc( &g->d_dev_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
-  fd_work_carve( &g->dev_work, g->d_dev_work_base, max_sigs );
-  HIPCHK( hipEventCreateWithFlags( &g->dev_done, hipEventDisableTiming ) );
-  HIPCHK( hipEventRecord( g->dev_done, g->slot[0].stream ) );
+  HIPCHK( hipStreamCreateWithFlags( &g->dev_sf, hipStreamNonBlocking ) );
+  {
+    /* the DSM stream at the highest priority: as the pool's waves retire,
+       its own next waves are dispatched first and the next launch's front
+       end only fills what it leaves idle (its last round) */
+    int lo = 0, hi = 0;
+    if( hipDeviceGetStreamPriorityRange( &lo, &hi ) != hipSuccess ) { (void)hipGetLastError(); lo = hi = 0; }
+    char const * pe = getenv( "FD_ED25519_GPU_DSM_PRIO" );   /* experiments: 0 = default priority */
+    if( pe && !atoi( pe ) ) hi = 0;
+    HIPCHK( hipStreamCreateWithPriority( &g->dev_sb, hipStreamNonBlocking, hi ) );
+  }
+  for( int b=0; b<2; b++ ) {
+    HIPCHK( hipMalloc( &g->d_dev_work_base[b], FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
+    fd_work_carve( &g->dev_work[b], g->d_dev_work_base[b], max_sigs );
+    HIPCHK( hipEventCreateWithFlags( &g->dev_in[b],    hipEventDisableTiming ) );
+    HIPCHK( hipEventCreateWithFlags( &g->dev_front[b], hipEventDisableTiming ) );
+    HIPCHK( hipEventCreateWithFlags( &g->dev_back[b],  hipEventDisableTiming ) );
+    HIPCHK( hipEventRecord( g->dev_back[b], g->dev_sb ) );
+  }
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
   return g;
 fail:
@@ -304,10 +329,12 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
         return;
       }
   }
-  if( g->dev_done && fd_wait_query( fd_event_query, (void *)g->dev_done, FD_POLL_SPIN_NS, to ) != 1 ) {
-    snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
-    return;
-  }
+  hipStream_t dsts[2] = { g->dev_sf, g->dev_sb };
+  for( int k=0; k<2; k++ )
+    if( dsts[k] && fd_wait_query( fd_stream_query, (void *)dsts[k], FD_POLL_SPIN_NS, to ) != 1 ) {
+      snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
+      return;
+    }
   for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p ) hipHostUnregister( (void *)g->reg[k].p );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
@@ -323,8 +350,16 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     if( sl->stream ) hipStreamDestroy( sl->stream );
     if( sl->done   ) hipEventDestroy( sl->done );
   }
-  if( g->dev_done ) hipEventDestroy( g->dev_done );
-  if( g->d_dev_work_base ) hipFree( g->d_dev_work_base );
+  for( int i=0; i<FD_DEV_STATS_MAX; i++ )
+    for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->dev_ev[i][k] ) hipEventDestroy( g->dev_ev[i][k] );
+  for( int b=0; b<2; b++ ) {
+    if( g->dev_in[b]    ) hipEventDestroy( g->dev_in[b] );
+    if( g->dev_front[b] ) hipEventDestroy( g->dev_front[b] );
+    if( g->dev_back[b]  ) hipEventDestroy( g->dev_back[b] );
+    if( g->d_dev_work_base[b] ) hipFree( g->d_dev_work_base[b] );
+  }
+  if( g->dev_sf ) hipStreamDestroy( g->dev_sf );
+  if( g->dev_sb ) hipStreamDestroy( g->dev_sb );
   for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->kev[k] ) hipEventDestroy( g->kev[k] );
   delete g;
 }
@@ -451,29 +486,108 @@ extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? 
 
 /* The device-resident path.  Descriptors are bounds-checked on the device
    against blob_sz (fd_k_prep reports FD_ED25519_ERR_ARG, nothing reads
-   outside the blob).  Launches serialise on the engine's device-resident
-   working set: each waits (on the device) for the previous one, whatever
-   stream either came on. */
+   outside the blob).  Launch k takes working set b = k mod 2:
+     stream: record dev_in[b]
+     dev_sf: wait dev_in[b] (inputs ready), wait dev_back[b] (launch k-2
+             done with set b); front part; record dev_front[b]
+     dev_sb: wait dev_front[b]; back part (DSM, codes to d_out); record dev_back[b]
+     stream: wait dev_back[b]
+   so the caller's stream sees the codes in order, and launch k's front
+   end overlaps launch k-1's DSM (its tail: the pool's last round of
+   waves, ~0.9 ms per 1M-signature launch, tools/pool_rounds.py). */
 static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
-                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, hipEvent_t const * ev ) {
+                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, int flags ) {
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  if( (e = hipStreamWaitEvent( st, g->dev_done, 0 )) != hipSuccess ) return fd_gpu_fail( "hipStreamWaitEvent", e );
-  e = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work, (int32_t *)d_out, st, ev,
-                                   g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0),
-                                   g->pool_min, g->quad_max );
-  if( e != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e );
-  if( (e = hipEventRecord( g->dev_done, st )) != hipSuccess ) return fd_gpu_fail( "hipEventRecord", e );
+  int b = (int)(g->dev_seq & 1UL);
+  int mode = g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
+  fd_ed25519_gpu_work_t const * w = &g->dev_work[b];
+  hipEvent_t const * ev = NULL;
+  if( g->dev_stats_on && g->dev_stats_cnt < FD_DEV_STATS_MAX ) {
+    if( !g->dev_ev[g->dev_stats_cnt][0] )
+      for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ )
+        if( (e = hipEventCreate( &g->dev_ev[g->dev_stats_cnt][k] )) != hipSuccess ) return fd_gpu_fail( "hipEventCreate", e );
+    ev = g->dev_ev[g->dev_stats_cnt++];
+  }
+  /* inputs: ordered after the work already on the caller's stream --
+     which includes its wait for the previous launch's codes, so the front
+     end cannot start early -- unless the caller vouches that they are
+     complete (FD_ED25519_GPU_DEV_INPUTS_READY), which lets this launch's
+     front end overlap the previous launch's DSM */
+  if( !(flags & FD_ED25519_GPU_DEV_INPUTS_READY) )
+    if( (e = hipEventRecord( g->dev_in[b], st )) != hipSuccess
+     || (e = hipStreamWaitEvent( g->dev_sf, g->dev_in[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (inputs)", e );
+  if( (e = hipStreamWaitEvent( g->dev_sf, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (front)", e );
+  if( (e = fd_ed25519_gpu_launch_front( n, (uint8_t const *)d_blob, blob_sz, d_desc, w, g->dev_sf, ev, mode, g->pool_min, g->quad_max )) != hipSuccess )
+    return fd_gpu_fail( "fd_ed25519_gpu_launch_front", e );
+  if( (e = hipEventRecord( g->dev_front[b], g->dev_sf )) != hipSuccess
+   || (e = hipStreamWaitEvent( g->dev_sb, g->dev_front[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (back)", e );
+  if( (e = fd_ed25519_gpu_launch_back( n, (uint8_t const *)d_blob, d_desc, w, (int32_t *)d_out, g->dev_sb, ev, mode, g->pool_min, g->quad_max )) != hipSuccess )
+    return fd_gpu_fail( "fd_ed25519_gpu_launch_back", e );
+  if( (e = hipEventRecord( g->dev_back[b], g->dev_sb )) != hipSuccess
+   || (e = hipStreamWaitEvent( st, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (caller)", e );
+  g->dev_seq++;
   return 0;
+}
+
+/* Per-kernel durations of the pipelined launches issued between begin
+   and end (at most FD_DEV_STATS_MAX), each kernel bracketed by HIP events
+   on the stream it runs on -- measured while launches overlap, so a
+   kernel's duration includes any slow-down from the next launch's front
+   end sharing its SIMDs.  end() blocks until those launches are done and
+   writes the per-kernel SUM (ms) in fd_ed25519_gpu_verify_dev_timed's
+   phase order and the launch count. */
+extern "C" int fd_ed25519_gpu_dev_stats_begin( fd_ed25519_gpu_t * g ) {
+  if( !g ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->dev_lock );
+  g->dev_stats_on = 1; g->dev_stats_cnt = 0;
+  return 0;
+}
+extern "C" int fd_ed25519_gpu_dev_stats_end( fd_ed25519_gpu_t * g, float * kernel_ms_sum, unsigned long * launches ) {
+  if( !g || !kernel_ms_sum || !launches ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->dev_lock );
+  g->dev_stats_on = 0;
+  for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) kernel_ms_sum[k] = 0.f;
+  *launches = g->dev_stats_cnt;
+  hipError_t e;
+  for( unsigned long i=0; i<g->dev_stats_cnt; i++ ) {
+    int err = fd_event_wait( g->dev_ev[i][FD_ED25519_GPU_KERNEL_CNT], g->timeout_ns );
+    if( err ) return err;
+    for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
+      float ms = 0.f;
+      if( (e = hipEventElapsedTime( &ms, g->dev_ev[i][k], g->dev_ev[i][k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
+      kernel_ms_sum[k] += ms;
+    }
+  }
+  return 0;
+}
+
+/* a serial device-resident operation on `st` using working set 0: waits
+   for every earlier pipelined launch, and later ones wait for it */
+static hipError_t fd_dev_serial_begin( fd_ed25519_gpu_t * g, hipStream_t st ) {
+  hipError_t e;
+  for( int b=0; b<2; b++ ) if( (e = hipStreamWaitEvent( st, g->dev_back[b], 0 )) != hipSuccess ) return e;
+  return hipSuccess;
+}
+static hipError_t fd_dev_serial_end( fd_ed25519_gpu_t * g, hipStream_t st ) {
+  hipError_t e;
+  for( int b=0; b<2; b++ ) if( (e = hipEventRecord( g->dev_back[b], st )) != hipSuccess ) return e;
+  return hipSuccess;
+}
+
+extern "C" int fd_ed25519_gpu_verify_dev_ex( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
+                                             fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, int flags ) {
+  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!d_blob || !d_desc || !d_out)) || (flags & ~FD_ED25519_GPU_DEV_INPUTS_READY) )
+    return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->dev_lock );
+  return fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, flags );
 }
 
 extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
                                           fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream ) {
-  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
-  if( !n ) return 0;
-  std::lock_guard<std::mutex> guard( g->dev_lock );
-  return fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, NULL );
+  return fd_ed25519_gpu_verify_dev_ex( g, n, d_blob, blob_sz, d_desc, d_out, stream, 0 );
 }
 
 extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
@@ -483,8 +597,16 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) kernel_ms[k] = 0.f;
   if( !n ) return 0;
   std::lock_guard<std::mutex> guard( g->dev_lock );
-  int err = fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, g->kev );
-  if( err ) return err;
+  /* serial, on the caller's stream, so each kernel's events bracket it alone */
+  hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
+  hipError_t e0 = hipSetDevice( g->device );
+  if( e0 != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e0 );
+  int mode = g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
+  if( (e0 = fd_dev_serial_begin( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
+  if( (e0 = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work[0], (int32_t *)d_out, st, g->kev,
+                                         mode, g->pool_min, g->quad_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
+  if( (e0 = fd_dev_serial_end( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
+  int err;
   if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], g->timeout_ns )) ) return err;
   hipError_t e;
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ )
@@ -644,20 +766,20 @@ extern "C" int fd_ed25519_gpu_debug_k( fd_ed25519_gpu_t * g, unsigned long n, vo
   memcpy( sl->h_blob, blob, blob_sz );
   memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
   memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
-  uint64_t * d_k = (uint64_t *)g->dev_work.tab;   /* 1536 B of table scratch per signature >= 32 */
+  uint64_t * d_k = (uint64_t *)g->dev_work[0].tab;   /* 1536 B of table scratch per signature >= 32 */
   uint64_t * h_k = (uint64_t *)malloc( 32UL * n );
   int32_t * h_st = (int32_t *)malloc( 4UL * n );
   int err = 0;
   if( !h_k || !h_st ) { err = FD_ED25519_ERR_GPU; goto done; }
-  if( (e = hipStreamWaitEvent( st, g->dev_done, 0 )) != hipSuccess
+  if( (e = fd_dev_serial_begin( g, st )) != hipSuccess
    || (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess
    || (e = hipMemsetAsync( d_k, 0, 32UL * n, st )) != hipSuccess
-   || (e = fd_ed25519_gpu_launch_prep_k( n, sl->d_blob, blob_sz, (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff), &g->dev_work, d_k, st )) != hipSuccess
+   || (e = fd_ed25519_gpu_launch_prep_k( n, sl->d_blob, blob_sz, (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff), &g->dev_work[0], d_k, st )) != hipSuccess
    || (e = hipMemcpyAsync( h_k, d_k, 32UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
-   || (e = hipMemcpyAsync( h_st, g->dev_work.status, 4UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
+   || (e = hipMemcpyAsync( h_st, g->dev_work[0].status, 4UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
    || (e = hipEventRecord( sl->done, st )) != hipSuccess
-   || (e = hipEventRecord( g->dev_done, st )) != hipSuccess ) { err = fd_gpu_fail( "debug_k", e ); (void)hipStreamSynchronize( st ); goto done; }
-  if( (err = fd_event_wait( g->dev_done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; goto done; }
+   || (e = fd_dev_serial_end( g, st )) != hipSuccess ) { err = fd_gpu_fail( "debug_k", e ); (void)hipStreamSynchronize( st ); goto done; }
+  if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; goto done; }
   for( unsigned long i=0; i<n; i++ ) {
     status_out[i] = h_st[i];
     for( int j=0; j<4; j++ ) {

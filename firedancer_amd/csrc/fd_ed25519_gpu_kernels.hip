@@ -1270,14 +1270,16 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
   return hipMemcpyToSymbol( HIP_SYMBOL(fd_gpu_bi_tab), bi, sizeof(bi) );
 }
 
-extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
-                                                    fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                    hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
+/* The front part of a launch: op-stream reset, prep and decomp (one
+   fd_k_front launch on the latency schedule) and, on the pooled
+   schedule, the Ai tables (fd_k_dsm_setup).  Timing events ev[0..3]. */
+extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                                   fd_ed25519_gpu_work_t const * w, hipStream_t stream,
+                                                   hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
-  int flags = mode & ~0xff; mode &= 0xff;
+  mode &= 0xff;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
-  mode |= flags;
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
@@ -1298,11 +1300,30 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
     hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
   }
   if( ev ) hipEventRecord( ev[2], stream );
-  /* phases 3-5: DSM setup (Ai tables), DSM main loop, final compare; the
-     uniform schedule is one kernel (its time lands in phase 4) */
+  if( n >= pool_min ) {
+    hipLaunchKernelGGL( fd_k_dsm_setup, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->tab, portable );
+    if( ev ) hipEventRecord( ev[3], stream );
+  }
+  return hipGetLastError();
+}
+
+/* The back part: the DSM main loop and the compare (pooled: fd_k_dsm_pool
+   + fd_k_dsm_final; latency: the quad DSM; between: the uniform DSM).
+   Timing events ev[3..5]. */
+extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                                  fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                                  hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
+  if( !n ) return hipSuccess;
+  int flags = mode & ~0xff; mode &= 0xff;
+  int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
+  int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
+  unsigned nb  = (unsigned)((n + 255) / 256);
+  int quad = n < pool_min && !portable && n <= quad_max;
   if( n >= pool_min ) {
     uint32_t nw = (uint32_t)((n + FD_POOL - 1) / FD_POOL);  /* one full pool per wave */
-    hipLaunchKernelGGL( fd_k_dsm_setup, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->tab, portable );
+    /* again on this stream: with the front part on another stream (the
+       pipelined device-resident path) the pool's events must both be on
+       the stream it runs on */
     if( ev ) hipEventRecord( ev[3], stream );
     hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
                         w->tab, w->pts, portable, nw );
@@ -1310,7 +1331,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
   } else if( quad ) {
     if( ev ) hipEventRecord( ev[3], stream );
-    if( mode & FD_ED25519_GPU_LAUNCH_QUAD2 )
+    if( flags & FD_ED25519_GPU_LAUNCH_QUAD2 )
       hipLaunchKernelGGL( fd_k_dsm_quad2, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
                           n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
     else
@@ -1325,6 +1346,15 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   }
   if( ev ) hipEventRecord( ev[5], stream );
   return hipGetLastError();
+}
+
+/* both parts in order on one stream */
+extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                                    fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                                    hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
+  hipError_t e = fd_ed25519_gpu_launch_front( n, blob, blob_sz, desc, w, stream, ev, mode, pool_min, quad_max );
+  if( e != hipSuccess ) return e;
+  return fd_ed25519_gpu_launch_back( n, blob, desc, w, out, stream, ev, mode, pool_min, quad_max );
 }
 
 /* diagnostics: fd_k_prep alone, writing each pending signature's k as

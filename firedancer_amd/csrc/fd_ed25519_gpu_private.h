@@ -43,6 +43,12 @@ hipError_t fd_ed25519_gpu_upload_tables( void );
 hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                         fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                         hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                        fd_ed25519_gpu_work_t const * w, hipStream_t stream,
+                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
+                                       fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                       hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
 hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                          fd_ed25519_gpu_work_t const * w, uint64_t * kout, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,

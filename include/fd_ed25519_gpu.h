@@ -136,12 +136,16 @@ fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t *            gpu,
                               int *                         out );
 
 /* Device-resident: d_blob (blob_sz bytes, followed by >= 16 readable
-   pad bytes), d_desc and d_out are device pointers; enqueued on `stream`
-   (a hipStream_t, NULL for the engine's own stream); no host
-   synchronisation.  Descriptors are bounds-checked against blob_sz on the
-   device.  The device-resident path has its own HBM working set (it never
-   shares scratch with ring batches); successive calls are ordered on the
-   device whatever streams they are issued on. */
+   pad bytes), d_desc and d_out are device pointers; `stream` (a
+   hipStream_t, NULL for the engine's own stream) is ordered before and
+   after the launch (the kernels themselves run on the engine's two
+   device-resident streams); no host synchronisation.  Descriptors are
+   bounds-checked against blob_sz on the device.  The device-resident path
+   has two HBM working sets of its own (never shared with ring batches):
+   successive launches alternate between them, so launch k's front end
+   (SHA-512, decompression, tables) overlaps launch k-1's double-scalar
+   multiplication; codes land in d_out in order, visible to work issued
+   on `stream` after the call. */
 int
 fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
                            unsigned long                 n,
@@ -150,6 +154,23 @@ fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t *            gpu,
                            fd_ed25519_gpu_desc_t const * d_desc,
                            int *                         d_out,
                            void *                        stream );
+
+/* As fd_ed25519_gpu_verify_dev; flags FD_ED25519_GPU_DEV_INPUTS_READY:
+   the caller guarantees d_blob and d_desc are complete on the device when
+   the call is made (e.g. resident inputs uploaded and synchronised once),
+   so the launch need not wait for the work already queued on `stream` --
+   which includes that stream's wait for the previous launch's codes --
+   and its front end can overlap the previous launch's DSM. */
+#define FD_ED25519_GPU_DEV_INPUTS_READY (1)
+int
+fd_ed25519_gpu_verify_dev_ex( fd_ed25519_gpu_t *            gpu,
+                              unsigned long                 n,
+                              void const *                  d_blob,
+                              unsigned long                 blob_sz,
+                              fd_ed25519_gpu_desc_t const * d_desc,
+                              int *                         d_out,
+                              void *                        stream,
+                              int                           flags );
 
 /* Asynchronous pipeline over the engine's pinned host rings: submit
    copies the batch into a free pinned slot (descriptors packed after the
@@ -291,6 +312,15 @@ fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t *            gpu,
                                  float *                       kernel_ms );
 
 int fd_ed25519_gpu_kernel_cnt( void );
+
+/* Per-kernel durations of device-resident launches as they run in the
+   pipeline (fd_ed25519_gpu_verify_dev overlaps launch k's front end with
+   launch k-1's DSM): between begin and end, up to 64 launches get HIP
+   events around each kernel on the stream it runs on; end blocks until
+   they are done and writes the per-kernel sums (ms, the order of
+   fd_ed25519_gpu_verify_dev_timed) and the number of launches timed. */
+int fd_ed25519_gpu_dev_stats_begin( fd_ed25519_gpu_t * gpu );
+int fd_ed25519_gpu_dev_stats_end  ( fd_ed25519_gpu_t * gpu, float * kernel_ms_sum, unsigned long * launches );
 
 /* Device the engine runs on; last HIP error string (diagnostics). */
 int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );

@@ -29,7 +29,6 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("FD_ED25519_NO_TORCH", "1")
 
 from firedancer_amd import corpus  # noqa: E402
 
@@ -76,6 +75,8 @@ def ref_codes(L, b, threads=8):
 
 
 def main():
+    # (the product library is only the signer here; importing this module
+    # from the GPU tests must not change how the library loads)
     L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libfdref.so"))
     res = {"generator": "tests/golden/make_config_digests.py", "checker": "oracle/_ref/libfdref.so (reference AVX2 build)"}
     b = c1_batch()

@@ -266,3 +266,26 @@ def test_cu_groups_depth8_ring_vs_reference(ref):
             _check(out, x)
     finally:
         e.close()
+
+
+def test_verify_dev_pipelined_back_to_back(engine, ref):
+    """successive device-resident launches with inputs_ready overlap (launch
+    k's front end with launch k-1's DSM on the engine's two working sets);
+    eight back-to-back launches of four different batches into four
+    outputs, every code the reference's"""
+    torch = pytest.importorskip("torch")
+    bs = [corpus.adversarial(20000 + 3000 * k, 128, seed=300 + k, invalid_frac=0.2) for k in range(4)]
+    exps = [oracle_batch(ref, b) for b in bs]
+    ins = []
+    for b in bs:
+        ins.append((torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).cuda(),
+                    torch.from_numpy(b.desc.view(np.uint8).copy()).cuda(),
+                    torch.full((len(b),), 99, dtype=torch.int32, device="cuda")))
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream().cuda_stream
+    for r in range(2):
+        for (blob, desc, out), b in zip(ins, bs):
+            engine.verify_dev(len(b), blob.data_ptr(), len(b.blob), desc.data_ptr(), out.data_ptr(), s, inputs_ready=True)
+    torch.cuda.synchronize()
+    for (_, _, out), e in zip(ins, exps):
+        _check(out.cpu().numpy(), e)
