@@ -1024,6 +1024,18 @@ FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
 #endif
 struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS accesses (64 banks) */
 
+#ifdef FD_POOL_STAMPS
+/* diagnostic builds only (tools/pool_stamps.py): per wave, s_memtime cycles
+   spent in selection (loop top -> stepping lanes known) and in the step
+   (state load, math, store, owner update), split by op kind, and the
+   iteration counts: [wave][8] = sel_dbl, step_dbl, n_dbl, sel_add,
+   step_add, n_add, lanes_stepped, total */
+__device__ unsigned long fd_pool_stamps[65536*8];
+extern "C" hipError_t fd_ed25519_gpu_pool_stamps( void * host, unsigned long bytes ) {
+  return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_pool_stamps), bytes, 0, hipMemcpyDeviceToHost );
+}
+#endif
+
 FD_DEV void fd_pool_ld( fe4 & vt, fd_pool_lds const & L, uint32_t s ) {
 #pragma unroll
   for( int k=0; k<20; k++ ) {
@@ -1074,7 +1086,14 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   fd_mem_fence();
 
   int lo_d = 0, lo_a = 0;   /* last selection bound per op kind */
+#ifdef FD_POOL_STAMPS
+  unsigned long ps[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+  unsigned long pt_start = __builtin_amdgcn_s_memtime();
+#endif
   for(;;) {
+#ifdef FD_POOL_STAMPS
+    unsigned long pt0 = __builtin_amdgcn_s_memtime();
+#endif
 #if FD_POOL_PRIO
     __builtin_amdgcn_s_setprio( 2 );          /* bookkeeping: issue ahead of the other wave's step math */
 #endif
@@ -1144,6 +1163,9 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 #if FD_POOL_PRIO
     __builtin_amdgcn_s_setprio( 0 );
 #endif
+#ifdef FD_POOL_STAMPS
+    unsigned long pt1 = __builtin_amdgcn_s_memtime();
+#endif
     if( act ) {
       int t = mm >> 8, op = mm & 255;
       uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
@@ -1169,7 +1191,16 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     if( (x0 >> lane) & 1ULL ) mt[0] = v0;
     if( (x1 >> lane) & 1ULL ) mt[1] = v1;
     fd_mem_fence();
+#ifdef FD_POOL_STAMPS
+    unsigned long pt2 = __builtin_amdgcn_s_memtime();
+    ps[kind ? 3 : 0] += pt1 - pt0; ps[kind ? 4 : 1] += pt2 - pt1; ps[kind ? 5 : 2] += 1; ps[6] += nc;
+#endif
   }
+#ifdef FD_POOL_STAMPS
+  ps[7] = __builtin_amdgcn_s_memtime() - pt_start;
+  if( lane == 0 && gw < 65536u )
+    for( int k=0; k<8; k++ ) fd_pool_stamps[(uint64_t)gw*8 + k] = ps[k];
+#endif
 }
 
 /* final p1p1 -> p2 and the compare (uniform kernel's tail), one lane per
