@@ -1031,6 +1031,10 @@ struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS ac
    iteration counts: [wave][8] = sel_dbl, step_dbl, n_dbl, sel_add,
    step_add, n_add, lanes_stepped, total */
 __device__ unsigned long fd_pool_stamps[65536*8];
+__device__ unsigned long fd_pool_stamps2[65536*4];   /* selection sub-phases: counts+kind, bound walk, permute */
+extern "C" hipError_t fd_ed25519_gpu_pool_stamps2( void * host, unsigned long bytes ) {
+  return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_pool_stamps2), bytes, 0, hipMemcpyDeviceToHost );
+}
 extern "C" hipError_t fd_ed25519_gpu_pool_stamps( void * host, unsigned long bytes ) {
   return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_pool_stamps), bytes, 0, hipMemcpyDeviceToHost );
 }
@@ -1088,6 +1092,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   int lo_d = 0, lo_a = 0;   /* last selection bound per op kind */
 #ifdef FD_POOL_STAMPS
   unsigned long ps[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+  unsigned long ps2[4] = { 0, 0, 0, 0 };
   unsigned long pt_start = __builtin_amdgcn_s_memtime();
 #endif
   for(;;) {
@@ -1108,6 +1113,9 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     int kind = nA >= 64u || nA == nL;          /* 1: additions, 0: doublings */
     uint64_t x0 = kind ? A0 : (L0 & ~A0), x1 = kind ? A1 : (L1 & ~A1);   /* candidates */
     uint32_t nc = (uint32_t)(__popcll( x0 ) + __popcll( x1 ));
+#ifdef FD_POOL_STAMPS
+    unsigned long pta = __builtin_amdgcn_s_memtime();
+#endif
     if( nc > 64u ) {
       /* the 64 candidates with the smallest t (furthest from the end of
          their streams): lo = largest bound with at most 64 candidates
@@ -1144,6 +1152,9 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       nc = 64u;
     }
     uint32_t n0 = (uint32_t)__popcll( x0 );
+#ifdef FD_POOL_STAMPS
+    unsigned long ptb = __builtin_amdgcn_s_memtime();
+#endif
 
     /* lane l steps the l-th selected slot (bank-0 slots first): the owners
        push (slot, t, op) forward to their stepping lanes (ds_permute; the
@@ -1194,12 +1205,15 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 #ifdef FD_POOL_STAMPS
     unsigned long pt2 = __builtin_amdgcn_s_memtime();
     ps[kind ? 3 : 0] += pt1 - pt0; ps[kind ? 4 : 1] += pt2 - pt1; ps[kind ? 5 : 2] += 1; ps[6] += nc;
+    ps2[0] += pta - pt0; ps2[1] += ptb - pta; ps2[2] += pt1 - ptb;
 #endif
   }
 #ifdef FD_POOL_STAMPS
   ps[7] = __builtin_amdgcn_s_memtime() - pt_start;
   if( lane == 0 && gw < 65536u )
     for( int k=0; k<8; k++ ) fd_pool_stamps[(uint64_t)gw*8 + k] = ps[k];
+  if( lane == 0 && gw < 65536u )
+    for( int k=0; k<4; k++ ) fd_pool_stamps2[(uint64_t)gw*4 + k] = ps2[k];
 #endif
 }
 

@@ -46,6 +46,14 @@ def main():
            "iters_per_wave": float((tot[2] + tot[5]) / nw), "add_iter_frac": float(tot[5] / (tot[2] + tot[5])),
            "lane_occupancy": float(tot[6] / (64 * (tot[2] + tot[5]))),
            "accepted": bool((d_out == 0).all().item())}
+    g = getattr(fa.lib(), "fd_ed25519_gpu_pool_stamps2", None)
+    if g is not None:
+        g.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
+        b2 = np.zeros(nw * 4, np.uint64)
+        assert g(b2.ctypes.data, b2.nbytes) == 0
+        t2 = b2.reshape(nw, 4).astype(np.float64).sum(0)
+        it = tot[2] + tot[5]
+        out.update(sel_counts_cycles=float(t2[0] / it), sel_walk_cycles=float(t2[1] / it), sel_permute_cycles=float(t2[2] / it))
     print(json.dumps(out), flush=True)
 
 
