@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--total", type=int, default=10_000_000)
     ap.add_argument("--chunk", type=int, default=1_000_000)
     ap.add_argument("--msg-sz", type=int, default=128)
+    ap.add_argument("--shape", choices=["packed", "txn"], default="packed",
+                    help="packed: sig|pub|msg of --msg-sz; txn: 1232-byte Solana legacy txns (msg 1167/1103 B, C2 shape)")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--schedules", default="pool,uniform,quad",
                     help="DSM schedules every chunk is verified under (all must match the reference)")
@@ -47,7 +49,8 @@ def main():
 
     ref = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libfdref.so"))
     P = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    eng = fa.Engine(0, max_sigs=a.chunk + 8, max_blob=a.chunk * (96 + a.msg_sz) + 4096, depth=1)
+    per_sig = corpus.TXN_MTU if a.shape == "txn" else 96 + a.msg_sz
+    eng = fa.Engine(0, max_sigs=a.chunk + 8, max_blob=a.chunk * per_sig + 4096, depth=1)
     ncase = len(corpus.CASES)
     agree = np.zeros(ncase, np.int64)
     seen = np.zeros(ncase, np.int64)
@@ -60,7 +63,10 @@ def main():
     while done < a.total:
         n = min(a.chunk, a.total - done)
         t0 = time.time()
-        b = corpus.adversarial(n, a.msg_sz, seed=100 + k, invalid_frac=0.1, nthreads=a.threads)
+        if a.shape == "txn":
+            b = corpus.adversarial_txns(n, seed=300 + k, invalid_frac=0.1, nthreads=a.threads)
+        else:
+            b = corpus.adversarial(n, a.msg_sz, seed=100 + k, invalid_frac=0.1, nthreads=a.threads)
         if k == 0:
             q = corpus.from_triples([(bytes.fromhex(m), bytes.fromhex(s), bytes.fromhex(p)) for m, s, p in Q2])
             b = corpus.concat([b, q])
@@ -97,7 +103,8 @@ def main():
         print(f"chunk {k}: {done} sigs, mismatches so far {mism} {sched_mism}, gen {t1 - t0:.1f}s gpu {t2 - t1:.2f}s ref {t3 - t2:.1f}s",
               flush=True)
     res = {"config": "C3 adversarial corpus (BASELINE.json configs[2])", "signatures": int(seen.sum()),
-           "mismatches": mism, "bit_exact": mism == 0 and not any(sched_mism.values()), "msg_sz": a.msg_sz,
+           "mismatches": mism, "bit_exact": mism == 0 and not any(sched_mism.values()),
+           "shape": a.shape, "msg_sz": [1103, 1167] if a.shape == "txn" else a.msg_sz,
            "mismatches_by_dsm_schedule": sched_mism,
            "per_case": {corpus.CASES[c]: {"n": int(seen[c]), "agree": int(agree[c])} for c in range(ncase)},
            "reference_codes_by_case": hist,
