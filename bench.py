@@ -99,7 +99,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
-    ap.add_argument("--ring-depth", type=int, default=6, help="ring slots of the C2 streaming leg")
+    ap.add_argument("--ring-depth", type=int, default=8, help="ring slots of the C2 streaming leg")
+    ap.add_argument("--ring-window", type=int, default=5,
+                    help="batches in flight on the C2 streaming leg (below the depth: free slots on the least "
+                         "loaded CU group; 5 of 8 keeps p99 under 1 ms, profiles/r02_ring_sweep_window.jsonl)")
     ap.add_argument("--dry-cpu", action="store_true", help="rehearse the multi-rank plumbing on the CPU (tests only)")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -385,7 +388,10 @@ def main():
         if not a.no_latency:
             # C2 at its own granularity: 4096-signature batches through the
             # per-GPU feeder and pinned ring, PCIe both ways included
-            res["latency"] = ring_stream(fa, base, local, a.latency_batches, a.ring_depth)
+            res["latency"] = ring_stream(fa, base, local, a.latency_batches, a.ring_depth, window=a.ring_window)
+            # one more batch in flight: more throughput, p99 just above 1 ms
+            res["latency"]["throughput_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
+                                                             window=min(a.ring_window + 1, a.ring_depth))
             res["latency"]["lower_latency_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), 4)
             # one batch in flight at a time: the per-batch floor
             res["latency"]["depth1"] = ring_stream(fa, base, local, max(a.latency_batches // 5, 20), 1)

@@ -479,6 +479,17 @@ static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * bl
     if( sl->orphan && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->ticket = 0; }
   }
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && g->slot[s].h_blob == blob ) return &g->slot[s];
+  if( g->groups > 1 ) {
+    /* slot s runs on CU group s mod groups: of the free slots, take one on
+       the group with the fewest batches in flight, so a ring kept below
+       its depth spreads its batches evenly over the groups */
+    int cnt[FD_GPU_DEPTH_MAX] = { 0 };
+    for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket ) cnt[s % g->groups]++;
+    int best = -1;
+    for( int s=0; s<g->depth; s++ )
+      if( !g->slot[s].ticket && !g->slot[s].staged && (best < 0 || cnt[s % g->groups] < cnt[best % g->groups]) ) best = s;
+    return best < 0 ? NULL : &g->slot[best];
+  }
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) return &g->slot[s];
   return NULL;
 }

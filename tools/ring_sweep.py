@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--depths", default="3,4,6,8")
     ap.add_argument("--groups", default="1,2,3,4")
     ap.add_argument("--windows", default="1")
+    ap.add_argument("--window-abs", default="", help="comma list of absolute windows (batches in flight), instead of --windows")
     ap.add_argument("--no-register", action="store_true")
     ap.add_argument("--quad2", default="1", help="comma list of quad2 policies (0 never, 1 ring, 2 always)")
     a = ap.parse_args()
@@ -32,9 +33,12 @@ def main():
         for g in [int(x) for x in a.groups.split(",")]:
             if g > d:
                 continue
-            for w in [int(x) for x in a.windows.split(",")]:
+            wins = [int(x) for x in a.window_abs.split(",")] if a.window_abs else [int(x) * d for x in a.windows.split(",")]
+            for w in wins:
+                if w > d:
+                    continue
                 for q in [int(x) for x in a.quad2.split(",")]:
-                    r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w * d, register=not a.no_register, quad2=q)
+                    r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w, register=not a.no_register, quad2=q)
                     print(json.dumps(r), flush=True)
 
 
