@@ -158,6 +158,8 @@ def cpu_baseline(batch, nsig, threads):
     else:
         return None
     res["per_core"] = res["value"] / threads
+    # a 4096-signature batch on the CPU = the wall time of 4096 verifies on these cores
+    res["batch_4096_ms"] = 4096.0 / res["value"] * 1e3
     res["sample"] = (f"{nsig} signatures of the same C2 corpus (1232-byte txns, msg 1167/1103 B), "
                      f"{threads} host threads (all this job may use), {dt:.2f} s wall ({dt * threads:.1f} thread-s)")
     if res["kind"] == "reference" and os.path.exists(port):
