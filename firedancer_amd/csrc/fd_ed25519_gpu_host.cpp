@@ -482,12 +482,20 @@ static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * bl
   if( g->groups > 1 ) {
     /* slot s runs on CU group s mod groups: of the free slots, take one on
        the group with the fewest batches in flight, so a ring kept below
-       its depth spreads its batches evenly over the groups */
+       its depth spreads its batches evenly over the groups; among those,
+       the group whose newest batch is oldest (it frees its CUs first) */
     int cnt[FD_GPU_DEPTH_MAX] = { 0 };
-    for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket ) cnt[s % g->groups]++;
+    unsigned long newest[FD_GPU_DEPTH_MAX] = { 0 };
+    for( int s=0; s<g->depth; s++ ) {
+      unsigned long t = g->slot[s].ticket;
+      if( t ) { cnt[s % g->groups]++; if( t > newest[s % g->groups] ) newest[s % g->groups] = t; }
+    }
     int best = -1;
-    for( int s=0; s<g->depth; s++ )
-      if( !g->slot[s].ticket && !g->slot[s].staged && (best < 0 || cnt[s % g->groups] < cnt[best % g->groups]) ) best = s;
+    for( int s=0; s<g->depth; s++ ) {
+      if( g->slot[s].ticket || g->slot[s].staged ) continue;
+      int k = s % g->groups, b = best < 0 ? 0 : best % g->groups;
+      if( best < 0 || cnt[k] < cnt[b] || (cnt[k] == cnt[b] && newest[k] < newest[b]) ) best = s;
+    }
     return best < 0 ? NULL : &g->slot[best];
   }
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) return &g->slot[s];
