@@ -95,7 +95,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--step-batches", type=int, default=STEP_BATCHES)
-    ap.add_argument("--unique", type=int, default=UNIQUE_SIGS)
+    ap.add_argument("--unique", type=int, default=0,
+                    help="distinct signatures per GPU (0: one per signature of a step, so the timed launches "
+                         "never re-read an input that could sit in the 256 MB MALL)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
@@ -302,7 +304,7 @@ def main():
 
     n_step = a.step_batches * BATCH_SIGS
     t0 = time.time()
-    base = corpus.solana_txns(a.unique, seed=1000 + rank, nthreads=min(16, os.cpu_count() or 8))
+    base = corpus.solana_txns(a.unique or n_step, seed=1000 + rank, nthreads=min(16, os.cpu_count() or 8))
     batch = base.tile(int(math.ceil(n_step / len(base))))
     batch.desc = batch.desc[:n_step]
     gen_s = time.time() - t0
