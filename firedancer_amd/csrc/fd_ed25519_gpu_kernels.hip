@@ -40,9 +40,13 @@ typedef fd_gpu_fe4_t fe4;
    whichever table it comes from */
 __device__ static int32_t fd_gpu_bi_tab[8*FD_TAB_ENTRY];
 
-/* minimum waves per SIMD requested for fd_k_dsm (caps its VGPRs) */
+/* minimum waves per SIMD requested for fd_k_dsm (caps its VGPRs).  2: no
+   spills (3 capped it at 168 VGPRs with 11 spilled); the batches it serves
+   (32 K - 256 K signatures) are 1-4 waves per SIMD anyway.  A/B,
+   tools/midsize_ab.sh: 65,536 signatures 1.283 -> 1.245 ms, 131,072
+   2.227 -> 2.177 ms (profiles/r02_midsize_ab.txt) */
 #ifndef FD_DSM_WAVES
-#define FD_DSM_WAVES 3
+#define FD_DSM_WAVES 2
 #endif
 
 /* ------------------------------------------------------------------ */

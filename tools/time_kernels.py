@@ -1,6 +1,7 @@
 """Per-kernel HIP-event timing of one library build on the C2 workload
 (experiments: FD_ED25519_LIB=<variant.so> python tools/time_kernels.py).
-Prints prep/decomp/dsm ms averaged over reps; results are not checked."""
+Prints prep/decomp/dsm ms averaged over reps; results are not checked.
+usage: time_kernels.py [n (default 262144)] [dsm_pool_min (default: the engine's)]"""
 import math
 import os
 import sys
@@ -14,11 +15,13 @@ def main():
     import torch
     import firedancer_amd as fa
     from firedancer_amd import corpus
-    n = 64 * 4096
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 64 * 4096
     base = corpus.solana_txns(65536, seed=1000, nthreads=16)
     batch = base.tile(int(math.ceil(n / len(base))))
     batch.desc = batch.desc[:n]
     eng = fa.Engine(0, max_sigs=n, max_blob=max(len(batch.blob), 1 << 24))
+    if len(sys.argv) > 2:
+        eng.dsm_pool_min = int(sys.argv[2])
     dev = torch.device("cuda", 0)
     blob_sz = len(batch.blob)
     d_blob = torch.from_numpy(np.concatenate([batch.blob, np.zeros(64, np.uint8)])).to(dev)
@@ -33,7 +36,7 @@ def main():
         ks += eng.verify_dev_timed(n, d_blob.data_ptr(), blob_sz, d_desc.data_ptr(), d_out.data_ptr(), s)
     ks /= reps
     ok = bool((d_out == 0).all().item())
-    print(os.environ.get("FD_ED25519_LIB", "default"), " ".join(f"{k[5:]}={v:.4f}" for k, v in zip(fa.Engine.KERNELS, ks)),
+    print(os.environ.get("FD_ED25519_LIB", "default"), n, "pool_min", eng.dsm_pool_min, " ".join(f"{k[5:]}={v:.4f}" for k, v in zip(fa.Engine.KERNELS, ks)),
           "accepted" if ok else "NOT-ACCEPTED")
 
 
