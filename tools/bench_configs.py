@@ -105,8 +105,9 @@ def main():
     big, msg, _, _ = corpus.single_msg(1 << 18, 442, seed=7, nthreads=a.threads)
     eng = fa.Engine(0, max_sigs=1 << 18, max_blob=len(big.blob) + 4096)
     rate, codes = dev_throughput(eng, big, 10, torch)
-    res["throughput_2^18_signers_442B"] = {"verifies_per_s": rate, "all_accepted": bool((codes == 0).all()),
-                                           "inputs": "HBM-resident"}
+    e, _ = ref_codes(ref, big, a.threads)
+    res["throughput_2^18_signers_442B"] = {"verifies_per_s": rate, "mismatches_vs_reference": int((codes != e).sum()),
+                                           "reference_rejects": int((e != 0).sum()), "inputs": "HBM-resident"}
     res["bit_exact_vs_reference"] = True
     print(json.dumps(res), flush=True)
     eng.close()
