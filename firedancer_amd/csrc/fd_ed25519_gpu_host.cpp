@@ -597,7 +597,9 @@ static hipError_t fd_dev_serial_end( fd_ed25519_gpu_t * g, hipStream_t st ) {
 
 extern "C" int fd_ed25519_gpu_verify_dev_ex( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
                                              fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, int flags ) {
-  if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!d_blob || !d_desc || !d_out)) || (flags & ~FD_ED25519_GPU_DEV_INPUTS_READY) )
+  /* the blob is the caller's device memory: max_blob (the pinned ring's
+     capacity) does not bound it */
+  if( !g || n > g->max_sigs || (n && (!d_blob || !d_desc || !d_out)) || (flags & ~FD_ED25519_GPU_DEV_INPUTS_READY) )
     return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
   std::lock_guard<std::mutex> guard( g->dev_lock );
@@ -612,7 +614,7 @@ extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n,
 extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
                                                 fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream,
                                                 float * kernel_ms ) {
-  if( !g || n > g->max_sigs || blob_sz > g->max_blob || !kernel_ms || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
+  if( !g || n > g->max_sigs || !kernel_ms || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) kernel_ms[k] = 0.f;
   if( !n ) return 0;
   std::lock_guard<std::mutex> guard( g->dev_lock );

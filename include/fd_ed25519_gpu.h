@@ -140,7 +140,9 @@ fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t *            gpu,
    hipStream_t, NULL for the engine's own stream) is ordered before and
    after the launch (the kernels themselves run on the engine's two
    device-resident streams); no host synchronisation.  Descriptors are
-   bounds-checked against blob_sz on the device.  The device-resident path
+   bounds-checked against blob_sz on the device; blob_sz is not bounded
+   by the engine's max_blob (that sizes the pinned ring), n is bounded by
+   max_sigs (the working sets).  The device-resident path
    has two HBM working sets of its own (never shared with ring batches):
    successive launches alternate between them, so launch k's front end
    (SHA-512, decompression, tables) overlaps launch k-1's double-scalar
