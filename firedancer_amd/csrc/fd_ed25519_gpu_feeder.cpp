@@ -146,6 +146,7 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
   (void)hipSetDevice( fd_ed25519_gpu_device( f->gpu ) );
   int depth = fd_ed25519_gpu_depth( f->gpu );
   fd_ed25519_gpu_job_t * pending = NULL;          /* popped, waiting for a free slot */
+  unsigned long last = fd_feeder_now();           /* last progress */
   for(;;) {
     int progress = 0;
     /* keep the ring full */
@@ -161,8 +162,27 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
     }
     /* collect what finished, oldest first, without blocking */
     while( fd_feeder_collect( f ) ) progress = 1;
-    if( progress ) continue;
-    if( !f->inflight.empty() || !f->zombies.empty() ) {
+    if( progress ) { last = fd_feeder_now(); continue; }
+    if( pending && f->inflight.empty() ) {
+      /* no free slot and nothing of ours in flight: every slot is held by a
+         batch given up on (a wedged device).  Bounded like every other wait:
+         after the engine's timeout the queued jobs fail with ERR_GPU. */
+      long to = fd_ed25519_gpu_timeout( f->gpu );
+      if( to >= 0 && fd_feeder_now() - last > (unsigned long)to ) {
+        fd_job_finish( pending, FD_ED25519_ERR_GPU ); pending = NULL;
+        std::lock_guard<std::mutex> g( f->lock );
+        while( !f->queue.empty() ) { fd_job_finish( f->queue.front(), FD_ED25519_ERR_GPU ); f->queue.pop_front(); }
+        last = fd_feeder_now();
+        continue;
+      }
+    }
+    if( f->inflight.empty() && !pending && f->halt.load() ) {
+      /* halting: only batches given up on are left; the engine reclaims or
+         leaks their slots (fd_ed25519_gpu_delete) */
+      std::lock_guard<std::mutex> g( f->lock );
+      if( f->queue.empty() ) break;
+    }
+    if( !f->inflight.empty() || !f->zombies.empty() || pending ) {
       /* a batch is in flight and nothing else to do: a short pause, then
          poll again (the tile-style busy poll; one core per GPU) */
       __builtin_ia32_pause();

@@ -7,26 +7,32 @@
    descriptors outside the blob get FD_ED25519_ERR_ARG exactly as the
    device reports them.  Ring semantics follow fd_ed25519_gpu_host.cpp:
    a staged slot's buffers are the caller's zero-copy blob; a poll without
-   block reports "not yet" on every other ticket to exercise that path. */
+   block reports "not yet" on every other ticket to exercise that path.
+   For the feeder (fd_ed25519_gpu_feeder.cpp) it also provides the
+   engine's device / timeout accessors, the two HIP calls the feeder makes
+   (no GPU: no NUMA node, a no-op set-device), and a "wedged device" switch
+   (fake_engine_wedge): batches submitted while it is on never complete. */
 #include <stdlib.h>
 #include <string.h>
+#include <mutex>
 #include "fd_ed25519_gpu.h"
 #include "fd_ed25519_gpu_desc.h"
 
 extern "C" int oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
 
 #define FAKE_DEPTH_MAX 8
-struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket; int staged, polls; };
+struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket; int staged, polls, wedged; };
 struct fd_ed25519_gpu {
-  unsigned long max_sigs, max_blob, next; int depth;
+  unsigned long max_sigs, max_blob, next; int depth, wedge; long timeout_ns;
   fake_slot slot[ FAKE_DEPTH_MAX ];
+  std::mutex lock;
 };
 
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long max_sigs, unsigned long max_blob, int depth ) {
   (void)device;
   if( !max_sigs || depth < 1 || depth > FAKE_DEPTH_MAX ) return NULL;
-  fd_ed25519_gpu_t * g = (fd_ed25519_gpu_t *)calloc( 1, sizeof(*g) );
-  g->max_sigs = max_sigs; g->max_blob = max_blob; g->depth = depth; g->next = 1;
+  fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
+  g->max_sigs = max_sigs; g->max_blob = max_blob; g->depth = depth; g->next = 1; g->timeout_ns = 10000000000L;
   for( int s=0; s<depth; s++ ) {
     g->slot[s].blob = (uint8_t *)malloc( max_blob + 64UL );      /* exactly the engine's pinned blob + pad */
     g->slot[s].desc = (fd_ed25519_gpu_desc_t *)malloc( max_sigs * sizeof(fd_ed25519_gpu_desc_t) );
@@ -40,8 +46,15 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new( int device, unsigned long max_
 extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   if( !g ) return;
   for( int s=0; s<g->depth; s++ ) { free( g->slot[s].blob ); free( g->slot[s].desc ); free( g->slot[s].out ); }
-  free( g );
+  delete g;
 }
+extern "C" int  fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { (void)g; return 0; }
+extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? g->timeout_ns : -1; }
+extern "C" int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long ns ) { if( !g ) return FD_ED25519_ERR_ARG; g->timeout_ns = ns; return 0; }
+extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on ) { std::lock_guard<std::mutex> l( g->lock ); g->wedge = on; }
+/* the HIP calls of the feeder (C linkage, as hip_runtime_api.h declares them) */
+extern "C" int hipDeviceGetPCIBusId( char * bus, int len, int device ) { (void)bus; (void)len; (void)device; return 1; }
+extern "C" int hipSetDevice( int device ) { (void)device; return 0; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g->max_sigs; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g->max_blob; }
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g->depth; }
@@ -60,6 +73,7 @@ extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob 
 extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
                                       fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
   if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> l( g->lock );
   fake_slot * sl = NULL;
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && g->slot[s].blob == blob ) sl = &g->slot[s];
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) sl = &g->slot[s];
@@ -72,7 +86,7 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
                ? oracle_verify( sl->blob + d->msg_off, d->msg_sz, sl->blob + d->sig_off, sl->blob + d->pub_off )
                : FD_ED25519_ERR_ARG;
   }
-  sl->n = n; sl->staged = 0; sl->polls = 0;
+  sl->n = n; sl->staged = 0; sl->polls = 0; sl->wedged = g->wedge;
   sl->ticket = g->next++;
   *ticket = sl->ticket;
   return 0;
@@ -80,9 +94,11 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
 
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
   if( !g || !ticket ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> l( g->lock );
   for( int s=0; s<g->depth; s++ ) {
     fake_slot * sl = &g->slot[s];
     if( sl->ticket != ticket ) continue;
+    if( sl->wedged ) return 0;                                   /* never completes */
     if( !block && (ticket & 1UL) && !sl->polls++ ) return 0;   /* "still in flight" once */
     if( out ) memcpy( out, sl->out, sl->n * sizeof(int) );
     sl->ticket = 0;

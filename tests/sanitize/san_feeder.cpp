@@ -1,0 +1,122 @@
+/* san_feeder.cpp -- TEST INFRASTRUCTURE ONLY: the per-GPU feeder
+   (firedancer_amd/csrc/fd_ed25519_gpu_feeder.cpp, unmodified) over the CPU
+   fake engine, built with ASan/UBSan and separately with TSan.
+
+   1. two producer threads push 150 jobs each (random sizes, random
+      descriptors into one shared blob, ~2 % of them outside it); every
+      job's codes must equal the restatement's verdict on the ORIGINAL
+      descriptors (ERR_ARG for the bad ones): catches a misrouted batch, a
+      wrong rebase, or a race between the producers and the feeder thread;
+   2. a wedged device: jobs whose batches never complete fail with
+      ERR_GPU once the engine's timeout passes, a later job still runs on
+      the slot that is left, and with every slot held by a batch given up
+      on a queued job fails with ERR_GPU instead of waiting forever;
+   3. fd_ed25519_gpu_feeder_delete returns with given-up batches still on
+      the device.
+   Exit 0 and "ok" on success. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <thread>
+#include <vector>
+#include "fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_desc.h"
+
+extern "C" int  oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
+extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on );
+
+#define CHECK( c ) do { if( !(c) ) { fprintf( stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c ); exit( 1 ); } } while( 0 )
+#define CHECK_EQ( a, b ) do { long a_ = (long)(a), b_ = (long)(b); if( a_ != b_ ) { fprintf( stderr, "FAIL %s:%d: %s = %ld, expected %ld\n", __FILE__, __LINE__, #a, a_, b_ ); exit( 1 ); } } while( 0 )
+
+static unsigned long rng_state = 0x2545F4914F6CDD1DUL;
+static unsigned long rnd( unsigned long * s ) { *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17; return *s; }
+
+#define ITEMS   2048UL
+#define ITEM_SZ 224UL     /* sig 64 | pub 32 | msg up to 128 */
+#define MAXN    256UL
+
+struct job_buf {
+  fd_ed25519_gpu_job_t          job;
+  std::vector<fd_ed25519_gpu_desc_t> desc;
+  std::vector<int>              out, exp;
+};
+
+static void make_job( job_buf * jb, uint8_t const * blob, unsigned long blob_sz, unsigned long * s ) {
+  /* a job references a window of the blob no larger than a ring slot (the
+     feeder ships the span its descriptors cover) */
+  unsigned long n = 1 + rnd( s ) % MAXN, base = rnd( s ) % (ITEMS - MAXN);
+  jb->desc.resize( n ); jb->out.assign( n, 99 ); jb->exp.resize( n );
+  for( unsigned long i=0; i<n; i++ ) {
+    unsigned long it = base + rnd( s ) % MAXN;
+    fd_ed25519_gpu_desc_t d;
+    d.sig_off = (uint32_t)(it*ITEM_SZ); d.pub_off = (uint32_t)(it*ITEM_SZ + 64); d.msg_off = (uint32_t)(it*ITEM_SZ + 96);
+    d.msg_sz  = (uint32_t)(rnd( s ) % 129);
+    if( rnd( s ) % 50 == 0 ) d.msg_sz = (uint32_t)(blob_sz + (rnd( s ) & 0xffff));   /* outside the blob */
+    jb->desc[i] = d;
+    jb->exp[i] = fd_ed25519_desc_ok( &d, blob_sz )
+               ? oracle_verify( blob + d.msg_off, d.msg_sz, blob + d.sig_off, blob + d.pub_off )
+               : FD_ED25519_ERR_ARG;
+  }
+  memset( &jb->job, 0, sizeof(jb->job) );
+  jb->job.n = n; jb->job.blob = blob; jb->job.blob_sz = blob_sz; jb->job.desc = jb->desc.data(); jb->job.out = jb->out.data();
+}
+
+int main( void ) {
+  fd_ed25519_gpu_t * g = fd_ed25519_gpu_new_ex( 0, MAXN, MAXN * ITEM_SZ + 4096, 4 );
+  CHECK( g );
+  fd_ed25519_gpu_feeder_t * f = fd_ed25519_gpu_feeder_new( g, 1 );
+  CHECK( f );
+  CHECK( fd_ed25519_gpu_feeder_numa_node( f ) == -1 );          /* no GPU: not pinned */
+
+  unsigned long blob_sz = ITEMS * ITEM_SZ;
+  std::vector<uint8_t> blob( blob_sz + 64 );
+  unsigned long s0 = rng_state;
+  for( unsigned long i=0; i<blob.size(); i++ ) blob[i] = (uint8_t)rnd( &s0 );
+  /* a share of signatures with S < L so verification runs past the S check */
+  for( unsigned long it=0; it<ITEMS; it+=2 ) blob[it*ITEM_SZ + 63] &= 0x0f;
+
+  /* 1. two producers */
+  int const PER = 150;
+  std::vector<job_buf> jobs( 2 * PER );
+  std::vector<std::thread> th;
+  for( int p=0; p<2; p++ ) th.emplace_back( [&, p]() {
+    unsigned long s = 0x9E3779B97F4A7C15UL * (unsigned long)(p + 1);
+    for( int k=0; k<PER; k++ ) {
+      job_buf * jb = &jobs[(size_t)(p*PER + k)];
+      make_job( jb, blob.data(), blob_sz, &s );
+      CHECK( fd_ed25519_gpu_feeder_push( f, &jb->job ) == 0 );
+      if( k % 7 == 0 ) CHECK_EQ( fd_ed25519_gpu_job_wait( &jb->job, -1 ), 0 );   /* some synchronous */
+    }
+  } );
+  for( auto & t : th ) t.join();
+  unsigned long sigs = 0;
+  for( auto & jb : jobs ) {
+    CHECK_EQ( fd_ed25519_gpu_job_wait( &jb.job, 5000000000L ), 0 );
+    CHECK( jb.out == jb.exp );
+    CHECK( jb.job.t_done_ns >= jb.job.t_push_ns );
+    sigs += jb.job.n;
+  }
+
+  /* 2. a wedged device (the fake engine verifies inside submit, slowly
+     under the sanitizers, so the short timeout is only set here) */
+  fd_ed25519_gpu_set_timeout( g, 200000000L );                  /* 0.2 s */
+  unsigned long s = 77;
+  job_buf w[3];
+  fake_engine_wedge( g, 1 );
+  for( int k=0; k<3; k++ ) { make_job( &w[k], blob.data(), blob_sz, &s ); CHECK( fd_ed25519_gpu_feeder_push( f, &w[k].job ) == 0 ); }
+  for( int k=0; k<3; k++ ) CHECK_EQ( fd_ed25519_gpu_job_wait( &w[k].job, 5000000000L ), FD_ED25519_ERR_GPU );
+  job_buf a;
+  make_job( &a, blob.data(), blob_sz, &s );
+  CHECK( fd_ed25519_gpu_feeder_push( f, &a.job ) == 0 );
+  CHECK_EQ( fd_ed25519_gpu_job_wait( &a.job, 5000000000L ), FD_ED25519_ERR_GPU );   /* the 4th slot wedges too */
+  fake_engine_wedge( g, 0 );
+  job_buf b[2];
+  for( int k=0; k<2; k++ ) { make_job( &b[k], blob.data(), blob_sz, &s ); CHECK( fd_ed25519_gpu_feeder_push( f, &b[k].job ) == 0 ); }
+  for( int k=0; k<2; k++ ) CHECK_EQ( fd_ed25519_gpu_job_wait( &b[k].job, 5000000000L ), FD_ED25519_ERR_GPU );   /* no slot left */
+
+  /* 3. delete with every slot held by a batch given up on */
+  fd_ed25519_gpu_feeder_delete( f );
+  fd_ed25519_gpu_delete( g );
+  printf( "ok %lu signatures in %d jobs\n", sigs, 2 * PER );
+  return 0;
+}

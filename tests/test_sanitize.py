@@ -92,3 +92,17 @@ def test_libfuzzer(built, tmp_path, target, secs):
                        capture_output=True, text=True, env=env, timeout=secs + 120, cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "Done" in r.stderr and "ERROR" not in r.stderr
+
+
+def test_feeder_asan_and_tsan(built):
+    """The per-GPU feeder thread (fd_ed25519_gpu_feeder.cpp, unmodified) on the
+    fake engine: two producer threads' jobs get exactly their own codes
+    (ERR_ARG at out-of-blob descriptors), batches on a wedged device fail
+    with ERR_GPU after the engine timeout instead of blocking, a queued job
+    with every slot given up on fails the same way, and delete returns --
+    under ASan/UBSan and under ThreadSanitizer."""
+    env = dict(ENV, TSAN_OPTIONS="halt_on_error=1")
+    for exe in ("san_feeder", "tsan_feeder"):
+        r = subprocess.run([os.path.join(built, exe)], capture_output=True, env=env, timeout=240)
+        assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
+        assert r.stdout.startswith(b"ok "), exe
