@@ -100,9 +100,12 @@ def test_feeder_asan_and_tsan(built):
     (ERR_ARG at out-of-blob descriptors), batches on a wedged device fail
     with ERR_GPU after the engine timeout instead of blocking, a queued job
     with every slot given up on fails the same way, and delete returns --
-    under ASan/UBSan and under ThreadSanitizer."""
+    under ASan/UBSan and under ThreadSanitizer.  The one-process
+    multi-device path (fd_ed25519_gpu_multi.cpp on three fake engines'
+    feeders) returns every index's own code, chunked over slots smaller
+    than its shards."""
     env = dict(ENV, TSAN_OPTIONS="halt_on_error=1")
-    for exe in ("san_feeder", "tsan_feeder"):
+    for exe in ("san_feeder", "tsan_feeder", "san_multi", "tsan_multi"):
         r = subprocess.run([os.path.join(built, exe)], capture_output=True, env=env, timeout=240)
         assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
         assert r.stdout.startswith(b"ok "), exe
