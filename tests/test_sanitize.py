@@ -109,3 +109,23 @@ def test_feeder_asan_and_tsan(built):
         r = subprocess.run([os.path.join(built, exe)], capture_output=True, env=env, timeout=240)
         assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
         assert r.stdout.startswith(b"ok "), exe
+
+
+def test_tile_task_cnc_asan_and_tsan(built, ref, tmp_path):
+    """The verify tile task (fd_verify_tile_task.cpp) on the fake engine,
+    its run loop on one thread and the cnc driven from another: BOOT -> RUN,
+    every frag consumed under periodic backpressure, HALT -> flush -> BOOT,
+    a publish stream and counters equal to the single-threaded tile's, and
+    an unknown signal -> FAIL; under ASan/UBSan and ThreadSanitizer."""
+    from test_verify_tile import make_stream
+    frags = make_stream(800, 93, ref)
+    p = tmp_path / "frags.bin"
+    with open(p, "wb") as f:
+        f.write(struct.pack("<I", len(frags)))
+        for fr in frags:
+            f.write(struct.pack("<I", len(fr)) + fr)
+    env = dict(ENV, TSAN_OPTIONS="halt_on_error=1")
+    for exe in ("san_task", "tsan_task"):
+        r = subprocess.run([os.path.join(built, exe), str(p)], capture_output=True, env=env, timeout=300)
+        assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
+        assert r.stdout.startswith(b"ok "), exe
