@@ -54,6 +54,29 @@ K_BEGIN(k_xor) XOR32(c0) XOR32(c1) XOR32(c2) XOR32(c3) XOR32(c4) XOR32(c5) XOR32
 #define PERM(c) { unsigned t=(unsigned)c; asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(t) : "v"(a), "v"(b)); c=t; }
 K_BEGIN(k_perm) PERM(c0) PERM(c1) PERM(c2) PERM(c3) PERM(c4) PERM(c5) PERM(c6) PERM(c7) K_END
 
+// quad DSM mix (fd_k_dsm_quad): DPP lane permutations, VOP3-encoded selects
+// and 3-input adds vs their VOP2 forms, and the LDS-crossbar alternative
+#define DPPMOV(c) { unsigned t=(unsigned)c; asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(t)); c=t; }
+K_BEGIN(k_dpp_mov) DPPMOV(c0) DPPMOV(c1) DPPMOV(c2) DPPMOV(c3) DPPMOV(c4) DPPMOV(c5) DPPMOV(c6) DPPMOV(c7) K_END
+#define ADDDPP(c) { unsigned t=(unsigned)c; asm volatile("v_add_u32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(t) : "v"(a)); c=t; }
+K_BEGIN(k_add_dpp) ADDDPP(c0) ADDDPP(c1) ADDDPP(c2) ADDDPP(c3) ADDDPP(c4) ADDDPP(c5) ADDDPP(c6) ADDDPP(c7) K_END
+#define MOV32(c) { unsigned t=(unsigned)c; asm volatile("v_mov_b32 %0, %0" : "+v"(t)); c=t; }
+K_BEGIN(k_mov) MOV32(c0) MOV32(c1) MOV32(c2) MOV32(c3) MOV32(c4) MOV32(c5) MOV32(c6) MOV32(c7) K_END
+#define CND64(c) { unsigned t=(unsigned)c; asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(t) : "v"(a) : "s40","s41"); c=t; }
+K_BEGIN(k_cndmask_e64) CND64(c0) CND64(c1) CND64(c2) CND64(c3) CND64(c4) CND64(c5) CND64(c6) CND64(c7) K_END
+#define CND32(c) { unsigned t=(unsigned)c; asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(t) : "v"(a) : "vcc"); c=t; }
+K_BEGIN(k_cndmask_e32) CND32(c0) CND32(c1) CND32(c2) CND32(c3) CND32(c4) CND32(c5) CND32(c6) CND32(c7) K_END
+#define ADD3(c) { unsigned t=(unsigned)c; asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(t) : "v"(a), "v"(b)); c=t; }
+K_BEGIN(k_add3) ADD3(c0) ADD3(c1) ADD3(c2) ADD3(c3) ADD3(c4) ADD3(c5) ADD3(c6) ADD3(c7) K_END
+#define LSHLADD(c) { unsigned t=(unsigned)c; asm volatile("v_lshl_add_u32 %0, %0, 1, %1" : "+v"(t) : "v"(a)); c=t; }
+K_BEGIN(k_lshl_add32) LSHLADD(c0) LSHLADD(c1) LSHLADD(c2) LSHLADD(c3) LSHLADD(c4) LSHLADD(c5) LSHLADD(c6) LSHLADD(c7) K_END
+#define AND32(c) { unsigned t=(unsigned)c; asm volatile("v_and_b32 %0, %1, %0" : "+v"(t) : "v"(a)); c=t; }
+K_BEGIN(k_and) AND32(c0) AND32(c1) AND32(c2) AND32(c3) AND32(c4) AND32(c5) AND32(c6) AND32(c7) K_END
+#define SHL32(c) { unsigned t=(unsigned)c; asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(t)); c=t; }
+K_BEGIN(k_lshl) SHL32(c0) SHL32(c1) SHL32(c2) SHL32(c3) SHL32(c4) SHL32(c5) SHL32(c6) SHL32(c7) K_END
+#define SWZ(c) { unsigned t=(unsigned)c; asm volatile("ds_swizzle_b32 %0, %0 offset:swizzle(QUAD_PERM,1,0,3,2)\n\ts_waitcnt lgkmcnt(0)" : "+v"(t)); c=t; }
+K_BEGIN(k_ds_swizzle) SWZ(c0) SWZ(c1) SWZ(c2) SWZ(c3) SWZ(c4) SWZ(c5) SWZ(c6) SWZ(c7) K_END
+
 typedef void (*kfn)(unsigned*, unsigned);
 int main() {
   struct { const char *name; kfn f; int instr_per_op; } ks[] = {
@@ -64,6 +87,10 @@ int main() {
     {"v_add_co+addc (pair)", k_add_addc, 2},
     {"v_alignbit_b32", k_alignbit, 1}, {"v_bitop3_b32", k_bitop3, 1}, {"v_bfi_b32", k_bfi, 1},
     {"v_xor_b32", k_xor, 1}, {"v_perm_b32", k_perm, 1},
+    {"v_mov_b32", k_mov, 1}, {"v_mov_b32_dpp quad_perm", k_dpp_mov, 1}, {"v_add_u32_dpp quad_perm", k_add_dpp, 1},
+    {"v_cndmask_b32_e64 (sgpr)", k_cndmask_e64, 1}, {"v_cndmask_b32_e32 (vcc)", k_cndmask_e32, 1},
+    {"v_add3_u32", k_add3, 1}, {"v_lshl_add_u32", k_lshl_add32, 1}, {"v_and_b32", k_and, 1},
+    {"v_lshlrev_b32", k_lshl, 1}, {"ds_swizzle_b32 (+wait)", k_ds_swizzle, 1},
   };
   hipDeviceProp_t p; hipGetDeviceProperties(&p, 0);
   int cus = p.multiProcessorCount; double clk = p.clockRate * 1e3;
