@@ -10,8 +10,8 @@
        with the descriptors rebased to the span,
      - submits it (H2D, the kernels, D2H on the slot's stream),
      - and, while later jobs are staged and submitted, collects completed
-       batches oldest first, writing the codes to the job's out[] and
-       releasing its state word.
+       batches as they complete (any order: jobs are independent), writing
+       the codes to the job's out[] and releasing its state word.
    So with a ring of depth D, up to D batches are in flight and batch
    k+1's staging copy overlaps batch k's transfers and kernels.
 
@@ -116,26 +116,31 @@ static int fd_feeder_submit( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t *
   return 1;
 }
 
-/* collect the oldest in-flight batch: 1 collected (or failed), 0 not
-   yet.  A batch not done within the engine's timeout fails its job with
-   FD_ED25519_ERR_GPU; its slot is reclaimed if it ever completes. */
+/* collect every in-flight batch that has completed, in any order (a
+   batch that finished on a lightly loaded CU group is not held behind an
+   older one still running on a busier group; jobs are independent, each
+   with its own state word): the number collected (or failed).  A batch not
+   done within the engine's timeout fails its job with FD_ED25519_ERR_GPU;
+   its slot is reclaimed if it ever completes. */
 static int fd_feeder_collect( fd_ed25519_gpu_feeder_t * f ) {
   for( size_t k=0; k<f->zombies.size(); ) {
     if( fd_ed25519_gpu_poll( f->gpu, f->zombies[k], NULL, 0 ) != 0 ) { f->zombies[k] = f->zombies.back(); f->zombies.pop_back(); }
     else k++;
   }
-  if( f->inflight.empty() ) return 0;
-  fd_feeder_inflight x = f->inflight.front();
-  int r = fd_ed25519_gpu_poll( f->gpu, x.ticket, x.job->out, 0 );
-  if( r == 0 ) {
-    long to = fd_ed25519_gpu_timeout( f->gpu );
-    if( to < 0 || fd_feeder_now() - x.job->t_submit_ns <= (unsigned long)to ) return 0;
-    f->zombies.push_back( x.ticket );
-    r = FD_ED25519_ERR_GPU;
+  int done = 0;
+  long to = fd_ed25519_gpu_timeout( f->gpu );
+  for( auto it = f->inflight.begin(); it != f->inflight.end(); ) {
+    int r = fd_ed25519_gpu_poll( f->gpu, it->ticket, it->job->out, 0 );
+    if( r == 0 ) {
+      if( to < 0 || fd_feeder_now() - it->job->t_submit_ns <= (unsigned long)to ) { ++it; continue; }
+      f->zombies.push_back( it->ticket );
+      r = FD_ED25519_ERR_GPU;
+    }
+    fd_job_finish( it->job, r == 1 ? 1 : r );
+    it = f->inflight.erase( it );
+    done++;
   }
-  f->inflight.pop_front();
-  fd_job_finish( x.job, r == 1 ? 1 : r );
-  return 1;
+  return done;
 }
 
 static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
@@ -160,8 +165,8 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
       if( r == 0 ) break;
       pending = NULL; progress = 1;
     }
-    /* collect what finished, oldest first, without blocking */
-    while( fd_feeder_collect( f ) ) progress = 1;
+    /* collect what finished, without blocking */
+    if( fd_feeder_collect( f ) ) progress = 1;
     if( progress ) { last = fd_feeder_now(); continue; }
     if( pending && f->inflight.empty() ) {
       /* no free slot and nothing of ours in flight: every slot is held by a

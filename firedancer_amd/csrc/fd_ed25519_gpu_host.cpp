@@ -142,7 +142,7 @@ struct fd_ed25519_gpu {
   int           quad2;    /* FD_ED25519_GPU_QUAD2_*: when small batches take the 2-waves/SIMD quad DSM */
   int           ncu;
   struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
-  long          timeout_ns; /* bound on one blocking wait (< 0: none) */
+  long          timeout_ns; /* bound on one blocking wait (< 0: none); atomic: set from any thread, read by waiters and feeders */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   /* device-resident path (verify_dev / _timed): its own HBM working sets,
      so it never shares scratch with a ring batch */
@@ -163,6 +163,8 @@ struct fd_ed25519_gpu {
   hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
   std::mutex    lock;
 };
+
+static inline long fd_timeout( fd_ed25519_gpu_t const * g ) { return __atomic_load_n( &g->timeout_ns, __ATOMIC_RELAXED ); }
 
 #define HIPCHK(call) do { hipError_t e_ = (call); if( e_ != hipSuccess ) { fd_gpu_fail( #call, e_ ); goto fail; } } while(0)
 
@@ -237,7 +239,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
-  g->timeout_ns = FD_WAIT_TIMEOUT_NS_DEFAULT;
+  __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );
   /* measured slower on the ring at every depth (profiles/r02_ring_sweep_quad2.jsonl):
      one quad wave already keeps its SIMD busy */
   g->quad2 = FD_ED25519_GPU_QUAD2_NEVER;
@@ -320,7 +322,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   hipSetDevice( g->device );
   /* drain every stream, each wait bounded: if the device is wedged the
      engine's memory is leaked rather than freed under a running kernel */
-  long to = g->timeout_ns;
+  long to = fd_timeout( g );
   for( int s=0; s<g->depth; s++ ) {
     hipStream_t sts[2] = { g->slot[s].stream, g->slot[s].mstream };
     for( int k=0; k<2; k++ )
@@ -383,7 +385,16 @@ extern "C" int fd_ed25519_gpu_set_quad2( fd_ed25519_gpu_t * g, int policy ) {
   g->quad2 = policy;
   return 0;
 }
-extern "C" int fd_ed25519_gpu_quad2( fd_ed25519_gpu_t const * g ) { return g ? g->quad2 : -1; }
+/* the schedule knobs are set under the engine lock and read under it:
+   submitters, the device-resident path and the feeder thread may run
+   concurrently with a setter */
+struct fd_knobs { int mode; unsigned long pool_min, quad_max; int quad2; };
+static fd_knobs fd_knobs_get( fd_ed25519_gpu_t const * g ) {
+  std::lock_guard<std::mutex> guard( const_cast<fd_ed25519_gpu_t *>( g )->lock );
+  fd_knobs k = { g->mode, g->pool_min, g->quad_max, g->quad2 };
+  return k;
+}
+extern "C" int fd_ed25519_gpu_quad2( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).quad2 : -1; }
 
 /* Host regions the ring may DMA from directly (no staging copy): a batch
    whose blob lies inside one goes H2D straight from the caller's bytes
@@ -407,7 +418,7 @@ extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
   for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p == host ) {
     for( int s=0; s<g->depth; s++ ) {     /* no batch may still read from it */
       fd_ed25519_gpu_slot * sl = &g->slot[s];
-      if( sl->ticket && fd_event_wait( sl->done, g->timeout_ns ) ) return FD_ED25519_ERR_GPU;
+      if( sl->ticket && fd_event_wait( sl->done, fd_timeout( g ) ) ) return FD_ED25519_ERR_GPU;
     }
     hipError_t e = hipHostUnregister( host );
     g->reg[k].p = NULL; g->reg[k].sz = 0;
@@ -425,10 +436,10 @@ static int fd_registered( fd_ed25519_gpu_t const * g, void const * p, unsigned l
 extern "C" int fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long timeout_ns ) {
   if( !g ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
-  g->timeout_ns = timeout_ns;
+  __atomic_store_n( &g->timeout_ns, timeout_ns, __ATOMIC_RELAXED );
   return 0;
 }
-extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? g->timeout_ns : 0L; }
+extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? fd_timeout( g ) : 0L; }
 
 extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
   if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE && mode != FD_ED25519_GPU_MODE_STRICT) ) return FD_ED25519_ERR_ARG;
@@ -436,21 +447,21 @@ extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
   g->mode = mode;
   return 0;
 }
-extern "C" int fd_ed25519_gpu_mode( fd_ed25519_gpu_t const * g ) { return g ? g->mode : -1; }
+extern "C" int fd_ed25519_gpu_mode( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).mode : -1; }
 extern "C" int fd_ed25519_gpu_set_dsm_pool_min( fd_ed25519_gpu_t * g, unsigned long n ) {
   if( !g ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   g->pool_min = n;
   return 0;
 }
-extern "C" unsigned long fd_ed25519_gpu_dsm_pool_min( fd_ed25519_gpu_t const * g ) { return g ? g->pool_min : 0UL; }
+extern "C" unsigned long fd_ed25519_gpu_dsm_pool_min( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).pool_min : 0UL; }
 extern "C" int fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * g, unsigned long n ) {
   if( !g ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   g->quad_max = n;
   return 0;
 }
-extern "C" unsigned long fd_ed25519_gpu_dsm_quad_max( fd_ed25519_gpu_t const * g ) { return g ? g->quad_max : 0UL; }
+extern "C" unsigned long fd_ed25519_gpu_dsm_quad_max( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).quad_max : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
 
@@ -520,7 +531,8 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   int b = (int)(g->dev_seq & 1UL);
-  int mode = g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
+  fd_knobs kn = fd_knobs_get( g );
+  int mode = kn.mode | (kn.quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
   fd_ed25519_gpu_work_t const * w = &g->dev_work[b];
   hipEvent_t const * ev = NULL;
   if( g->dev_stats_on && g->dev_stats_cnt < FD_DEV_STATS_MAX ) {
@@ -538,11 +550,11 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
     if( (e = hipEventRecord( g->dev_in[b], st )) != hipSuccess
      || (e = hipStreamWaitEvent( g->dev_sf, g->dev_in[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (inputs)", e );
   if( (e = hipStreamWaitEvent( g->dev_sf, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (front)", e );
-  if( (e = fd_ed25519_gpu_launch_front( n, (uint8_t const *)d_blob, blob_sz, d_desc, w, g->dev_sf, ev, mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch_front( n, (uint8_t const *)d_blob, blob_sz, d_desc, w, g->dev_sf, ev, mode, kn.pool_min, kn.quad_max )) != hipSuccess )
     return fd_gpu_fail( "fd_ed25519_gpu_launch_front", e );
   if( (e = hipEventRecord( g->dev_front[b], g->dev_sf )) != hipSuccess
    || (e = hipStreamWaitEvent( g->dev_sb, g->dev_front[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (back)", e );
-  if( (e = fd_ed25519_gpu_launch_back( n, (uint8_t const *)d_blob, d_desc, w, (int32_t *)d_out, g->dev_sb, ev, mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch_back( n, (uint8_t const *)d_blob, d_desc, w, (int32_t *)d_out, g->dev_sb, ev, mode, kn.pool_min, kn.quad_max )) != hipSuccess )
     return fd_gpu_fail( "fd_ed25519_gpu_launch_back", e );
   if( (e = hipEventRecord( g->dev_back[b], g->dev_sb )) != hipSuccess
    || (e = hipStreamWaitEvent( st, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (caller)", e );
@@ -571,7 +583,7 @@ extern "C" int fd_ed25519_gpu_dev_stats_end( fd_ed25519_gpu_t * g, float * kerne
   *launches = g->dev_stats_cnt;
   hipError_t e;
   for( unsigned long i=0; i<g->dev_stats_cnt; i++ ) {
-    int err = fd_event_wait( g->dev_ev[i][FD_ED25519_GPU_KERNEL_CNT], g->timeout_ns );
+    int err = fd_event_wait( g->dev_ev[i][FD_ED25519_GPU_KERNEL_CNT], fd_timeout( g ) );
     if( err ) return err;
     for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
       float ms = 0.f;
@@ -622,13 +634,14 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e0 = hipSetDevice( g->device );
   if( e0 != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e0 );
-  int mode = g->mode | (g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
+  fd_knobs kn = fd_knobs_get( g );
+  int mode = kn.mode | (kn.quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
   if( (e0 = fd_dev_serial_begin( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   if( (e0 = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work[0], (int32_t *)d_out, st, g->kev,
-                                         mode, g->pool_min, g->quad_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
+                                         mode, kn.pool_min, kn.quad_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
   if( (e0 = fd_dev_serial_end( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   int err;
-  if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], g->timeout_ns )) ) return err;
+  if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], fd_timeout( g ) )) ) return err;
   hipError_t e;
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ )
     if( (e = hipEventElapsedTime( &kernel_ms[k], g->kev[k], g->kev[k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
@@ -717,7 +730,7 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   if( !sl ) return FD_ED25519_ERR_ARG;   /* every slot in flight or lent out */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
-  if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) {
+  if( (err = fd_event_wait( sl->done, fd_timeout( g ) )) ) {
     sl->ticket = g->next_ticket++;   /* still in flight: the slot is not reused until it drains */
     sl->orphan = 1;
     return err;
@@ -751,7 +764,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
   if( block ) {
-    int err = fd_event_wait( sl->done, g->timeout_ns );
+    int err = fd_event_wait( sl->done, fd_timeout( g ) );
     if( err ) return err;               /* timed out or failed; the ticket stays valid */
   } else {
     hipError_t e = hipEventQuery( sl->done );
@@ -800,7 +813,7 @@ extern "C" int fd_ed25519_gpu_debug_k( fd_ed25519_gpu_t * g, unsigned long n, vo
    || (e = hipMemcpyAsync( h_st, g->dev_work[0].status, 4UL * n, hipMemcpyDeviceToHost, st )) != hipSuccess
    || (e = hipEventRecord( sl->done, st )) != hipSuccess
    || (e = fd_dev_serial_end( g, st )) != hipSuccess ) { err = fd_gpu_fail( "debug_k", e ); (void)hipStreamSynchronize( st ); goto done; }
-  if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; goto done; }
+  if( (err = fd_event_wait( sl->done, fd_timeout( g ) )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; goto done; }
   for( unsigned long i=0; i<n; i++ ) {
     status_out[i] = h_st[i];
     for( int j=0; j<4; j++ ) {
@@ -842,7 +855,7 @@ extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long
   if( (e = hipMemcpyAsync( sl->h_dig, d_dig, n * 64UL, hipMemcpyDeviceToHost, sl->stream )) != hipSuccess )
     return fd_gpu_fail( "D2H digests", e );
   if( (e = hipEventRecord( sl->done, sl->stream )) != hipSuccess ) return fd_gpu_fail( "event", e );
-  int err = fd_event_wait( sl->done, g->timeout_ns );
+  int err = fd_event_wait( sl->done, fd_timeout( g ) );
   if( err ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
   unsigned long hsz = is384 ? 48UL : 64UL;
   for( unsigned long i=0; i<n; i++ ) memcpy( (uint8_t *)hash_out + i*hsz, sl->h_dig + i*64UL, hsz );
@@ -910,7 +923,7 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
     }
     int err = fd_slot_enqueue( g, sl, cnt, sl->h_blob, used, sl->h_desc );
     if( err ) return err;
-    if( (err = fd_event_wait( sl->done, g->timeout_ns )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
+    if( (err = fd_event_wait( sl->done, fd_timeout( g ) )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
     for( unsigned long k=0; k<cnt; k++ ) out[i+k] = sl->h_out[k];
     i += cnt;
   }

@@ -341,8 +341,9 @@ int fd_ed25519_gpu_device_cnt( void );
    (pin_numa), keeping the engine's ring full: a pushed job's descriptors
    are verified against its blob; the feeder copies the byte span they
    reference into a free ring slot (no copy for a registered region),
-   rebases the descriptors, submits, and collects completed batches oldest
-   first while later ones are staged.  Jobs complete in push order.
+   rebases the descriptors, submits, and collects batches as they
+   complete while later ones are staged.  Jobs are submitted in push order
+   but may complete out of it (wait on each job's own state).
 
    A job is owned by the caller; blob, desc and out must stay valid until
    its state is nonzero: 1 = codes in out[0..n), < 0 = FD_ED25519_ERR_*

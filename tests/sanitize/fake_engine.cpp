@@ -49,8 +49,8 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   delete g;
 }
 extern "C" int  fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { (void)g; return 0; }
-extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? g->timeout_ns : -1; }
-extern "C" int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long ns ) { if( !g ) return FD_ED25519_ERR_ARG; g->timeout_ns = ns; return 0; }
+extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? __atomic_load_n( &g->timeout_ns, __ATOMIC_RELAXED ) : -1; }
+extern "C" int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long ns ) { if( !g ) return FD_ED25519_ERR_ARG; __atomic_store_n( &g->timeout_ns, ns, __ATOMIC_RELAXED ); return 0; }
 extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on ) { std::lock_guard<std::mutex> l( g->lock ); g->wedge = on; }
 /* the HIP calls of the feeder (C linkage, as hip_runtime_api.h declares them) */
 extern "C" int hipDeviceGetPCIBusId( char * bus, int len, int device ) { (void)bus; (void)len; (void)device; return 1; }

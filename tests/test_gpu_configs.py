@@ -211,7 +211,8 @@ def test_feeder_stream_vs_reference(ref, register):
     """the per-GPU feeder (fd_ed25519_gpu_feeder) keeps a depth-6 ring full
     with 24 jobs of 1..4096 adversarial txn-shaped signatures (copied into
     the pinned ring, or DMA'd in place from a registered blob); every code
-    equals the reference's, jobs complete in push order"""
+    equals the reference's; each job's stamps are ordered push <= submit <=
+    done (jobs are collected as they complete, not in push order)"""
     b = corpus.adversarial_txns(4096 * 6, seed=123, invalid_frac=0.15)
     exp = oracle_batch(ref, b)
     e = fa.Engine(0, 4096, 8 << 20, depth=6)
@@ -233,11 +234,9 @@ def test_feeder_stream_vs_reference(ref, register):
             o = np.full(n, 99, np.int32)
             jobs.append((f.push(b.blob, d, o), lo, n))
             outs.append(o)
-        last = 0
         for (j, lo, n), o in zip(jobs, outs):
             f.wait(j)
-            assert j.t_done_ns >= last
-            last = j.t_done_ns
+            assert j.t_push_ns <= j.t_submit_ns <= j.t_done_ns
             _check(o, exp[lo:lo + n], None)
         f.close()
     finally:
