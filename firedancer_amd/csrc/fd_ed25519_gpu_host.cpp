@@ -20,6 +20,9 @@
 #include <string.h>
 #include <time.h>
 #include <mutex>
+#include <deque>
+#include <condition_variable>
+#include <vector>
 #include <atomic>
 #include "fd_ed25519_gpu_private.h"
 
@@ -959,15 +962,57 @@ extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned
   return r;
 }
 
+/* fd_ed25519_verify (fd_ed25519.h:96-101): one signature per call.  Calls
+   from several threads coalesce into shared batches (group commit): a call
+   joins the queue; if no batch is running it leads -- it takes every queued
+   call (up to FD_VQ_MAX) as one batch on the process-default engine, hands
+   each call its own code and wakes the rest; a call arriving while a batch
+   runs waits and rides the next one.  A lone caller waits for nothing
+   extra; N concurrent callers share one device round trip instead of
+   queueing N of them on the engine lock. */
+#define FD_VQ_MAX 4096UL
+struct fd_vreq { uint8_t const * m; unsigned long sz; uint8_t const * s; uint8_t const * p; int out; int done; };
+static std::mutex              fd_vq_lock;
+static std::condition_variable fd_vq_cv;
+static std::deque<fd_vreq *>   fd_vq;
+static int                     fd_vq_busy = 0;
+
+static void fd_vq_run( std::vector<fd_vreq *> const & b, std::vector<int> & code ) {
+  unsigned long n = b.size();
+  std::vector<uint8_t const *> m, s, p; std::vector<unsigned long> sz; std::vector<unsigned long> idx;
+  fd_ed25519_gpu_t * g = fd_default_engine();
+  unsigned long lim = g ? fd_ed25519_gpu_max_blob( g ) - 96UL : 0UL;
+  code.assign( n, FD_ED25519_ERR_GPU );
+  for( unsigned long k=0; k<n; k++ ) {
+    fd_vreq const * r = b[k];
+    if( !r->s || !r->p || (r->sz && !r->m) || (g && (r->sz > lim || r->sz > 0x7fffffffUL)) ) { code[k] = FD_ED25519_ERR_ARG; continue; }
+    m.push_back( r->m ); s.push_back( r->s ); p.push_back( r->p ); sz.push_back( r->sz ); idx.push_back( k );
+  }
+  if( idx.empty() ) return;
+  std::vector<int> out( idx.size() );
+  int err = fd_run_ptr_batch( idx.size(), m.data(), sz.data(), NULL, 0, s.data(), NULL, p.data(), NULL, out.data() );
+  for( unsigned long j=0; j<idx.size(); j++ ) code[idx[j]] = err ? err : out[j];
+}
+
 extern "C" int fd_ed25519_verify( void const * msg, unsigned long sz, void const * sig, void const * public_key, void * sha ) {
   (void)sha;
-  uint8_t const * m = (uint8_t const *)msg;
-  uint8_t const * s = (uint8_t const *)sig;
-  uint8_t const * p = (uint8_t const *)public_key;
-  int out = 0;
-  int err = fd_ed25519_verify_batch( 1UL, &m, &sz, &s, &p, &out );
-  if( err == FD_ED25519_ERR_GPU || err == FD_ED25519_ERR_ARG ) return err;
-  return out;
+  fd_vreq me = { (uint8_t const *)msg, sz, (uint8_t const *)sig, (uint8_t const *)public_key, 0, 0 };
+  std::unique_lock<std::mutex> lk( fd_vq_lock );
+  fd_vq.push_back( &me );
+  while( !me.done ) {
+    if( fd_vq_busy ) { fd_vq_cv.wait( lk ); continue; }
+    fd_vq_busy = 1;
+    std::vector<fd_vreq *> b;
+    while( !fd_vq.empty() && b.size() < FD_VQ_MAX ) { b.push_back( fd_vq.front() ); fd_vq.pop_front(); }
+    lk.unlock();
+    std::vector<int> code;
+    fd_vq_run( b, code );
+    lk.lock();
+    for( unsigned long k=0; k<b.size(); k++ ) { b[k]->out = code[k]; b[k]->done = 1; }
+    fd_vq_busy = 0;
+    fd_vq_cv.notify_all();
+  }
+  return me.out;
 }
 
 extern "C" char const * fd_ed25519_strerror( int err ) {

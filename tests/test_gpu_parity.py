@@ -152,6 +152,35 @@ def test_reference_shaped_apis(engine):
     assert out[100] != 0 and r == out[100] and (np.delete(out, 100) == 0).all()
 
 
+def test_per_signature_calls_concurrent(engine, ref):
+    """fd_ed25519_verify from 16 threads at once: the calls coalesce into
+    shared batches on the process-default engine (group commit), and every
+    call still returns its own signature's code, equal to the reference's;
+    a call with a message larger than the engine blob gets ERR_ARG without
+    failing the calls it shares a batch with."""
+    import threading
+    b = corpus.adversarial(16 * 48, 100, seed=18, invalid_frac=0.3)
+    exp = oracle_batch(ref, b)
+    msgs = [b.msg(i) for i in range(len(b))]
+    sigs = [b.sig(i) for i in range(len(b))]
+    pubs = [b.pub(i) for i in range(len(b))]
+    got = np.full(len(b), 99, np.int32)
+    big = [None]
+
+    def worker(t):
+        for i in range(t, len(b), 16):
+            got[i] = fa.verify(msgs[i], sigs[i], pubs[i])
+        if t == 0:
+            big[0] = fa.verify(bytes(1 << 27), sigs[0], pubs[0])
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert (got == exp).all()
+    assert big[0] == fa.ERR_ARG
+
+
 def test_async_ring(engine):
     """submit/poll over the pinned ring: depth batches in flight, each
     result identical to the synchronous path."""
