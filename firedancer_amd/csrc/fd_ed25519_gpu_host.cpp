@@ -143,6 +143,7 @@ struct fd_ed25519_gpu {
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           quad2;    /* FD_ED25519_GPU_QUAD2_*: when small batches take the 2-waves/SIMD quad DSM */
+  int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
   int           ncu;
   struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none); atomic: set from any thread, read by waiters and feeders */
@@ -247,6 +248,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
      one quad wave already keeps its SIMD busy */
   g->quad2 = FD_ED25519_GPU_QUAD2_NEVER;
   { char const * q2 = getenv( "FD_ED25519_GPU_QUAD2" ); if( q2 ) g->quad2 = atoi( q2 ); }   /* experiments */
+  { char const * ga = getenv( "FD_ED25519_GPU_GROUP_ALWAYS" ); g->group_always = ga && atoi( ga ); }  /* experiments */
   /* a slot's pinned and device blob buffers also hold the batch's
      descriptors, 16-aligned after the padded blob, so a batch is ONE H2D
      copy (a second small copy costs ~17 us of a ~0.75 ms 4096-signature
@@ -676,7 +678,7 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   /* the slot's CU group only while another ring batch is in flight (a
      lone batch runs faster spread over the whole device: depth-1 p50
      0.755 ms there vs 0.80 ms on a third of the CUs) */
-  int others = sl->mstream && n <= g->mask_max && fd_ring_busy( g, sl );
+  int others = sl->mstream && n <= g->mask_max && (g->group_always || fd_ring_busy( g, sl ));
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
   /* several ring batches in flight: the quad DSM at two waves per SIMD */
