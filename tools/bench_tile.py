@@ -38,10 +38,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    share = os.environ.get("FD_BENCH_SHARE_GPU") == "1"     # rehearsal: ranks share the visible GPUs
+    if share:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import firedancer_amd as fa
     from firedancer_amd import corpus, txn
     from firedancer_amd.tile import VerifyTile
@@ -99,7 +105,7 @@ def main():
     d0 = d0s[0]
     tot = np.array([sigs, pub, el])
     if dist:
-        t = torch.tensor(tot, dtype=torch.float64, device="cuda")
+        t = torch.tensor(tot, dtype=torch.float64, device="cpu" if share else "cuda")
         dist.all_reduce(t[:2])
         m = t[2:].clone()
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
