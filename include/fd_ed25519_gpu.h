@@ -77,6 +77,13 @@ fd_ed25519_verify_batch_single_msg( uint8_t const * msg,
 
 /* ---- Engine (the util/gpu shim) ----------------------------------------
 
+   No single reference function is replaced here: this is the util/gpu
+   shim the north star names.  Its asynchronous side follows the
+   reference's accelerator interface for the same path
+   (wd_ed25519_verify_req, src/wiredancer/c/wd_f1.h:104-113: requests
+   queued to the device, results collected later, polls bounded by
+   WD_TRY_LIMIT, wd_f1.h:25).
+
    A packed batch is one byte blob plus one descriptor per signature
    giving byte offsets into the blob: signature i is R||S at
    blob[sig_off..+64), its public key at blob[pub_off..+32) and its
