@@ -197,7 +197,8 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
 }
 
 /* (Re)create the slots' CU-masked streams: slot s runs on group s mod
-   groups (CU c in group c mod groups, so every group spans all XCDs).
+   groups, a contiguous range of logical CUs (physically spread over all
+   8 XCDs, disjoint from the other groups).
    groups <= 1 (or no CU masking on this runtime): every batch takes the
    whole device.  Slots must be idle. */
 static void fd_cu_groups_make( fd_ed25519_gpu_t * g, int groups ) {
@@ -210,7 +211,13 @@ static void fd_cu_groups_make( fd_ed25519_gpu_t * g, int groups ) {
   g->mask_max = groups > 1 ? 64UL * (unsigned long)(ncu / groups) : 0UL;
   for( int s=0; groups > 1 && s<g->depth; s++ ) {
     uint32_t mask[32] = { 0 };
-    for( int c=0; c<ncu; c++ ) if( c % groups == s % groups ) mask[c >> 5] |= 1u << (c & 31);
+    /* group k = logical CUs [k*ncu/groups, (k+1)*ncu/groups): measured on
+       MI355X (tools/cu_mask_probe.hip, profiles/r02_cu_mask_probe.txt)
+       such a mask puts a stream's waves on exactly ncu/groups physical CUs
+       spread over all 8 XCDs, disjoint from the other groups'; the
+       interleaved mask (CU c in group c mod groups) used before reached
+       all 256 physical CUs from every group -- no isolation at all */
+    for( int c=0; c<ncu; c++ ) if( c / (ncu / groups) == s % groups ) mask[c >> 5] |= 1u << (c & 31);
     if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess ) {
       (void)hipGetLastError();
       for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
@@ -275,12 +282,14 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
      latency schedule is lone waves (256 quad-DSM waves, 192 front-end
      waves); with several in flight, a batch's front end landed on the
      SIMDs of another batch's quad-DSM waves and ran at their pace (111 ->
-     ~250 us, tools/lat_trace3.py).  Up to FD_CU_GROUPS slots get disjoint
-     CU groups (CU c in group c mod groups, so every group spans all
-     XCDs); batches up to 64 signatures per group CU (one quad wave per
-     SIMD) run there while other ring batches are in flight (A/B, depth 3:
-     p50 0.914 -> 0.80 ms, p99 0.96 -> 0.84 ms), larger ones and lone
-     batches on the whole device. */
+     ~250 us, tools/lat_trace3.py, tools/front_stamps.py).  Up to
+     FD_CU_GROUPS slots get disjoint CU groups (fd_cu_groups_make);
+     batches up to 64 signatures per group CU (one quad wave per SIMD) run
+     there while other ring batches are in flight, larger ones and lone
+     batches on the whole device.  With groups that really are disjoint
+     (round 2: the interleaved masks of round 1 isolated nothing), the C2
+     ring at depth 8: 22.5 -> 26.3 M verifies/s at 5 in flight (p99 0.97
+     -> 0.83 ms), 28.5 M/s at p99 0.92 ms with 6 (profiles/r02_cu_groups_contiguous_ab.txt). */
   g->ncu = prop.multiProcessorCount;
   {
     /* groups scale with the ring up to 4 (64 CUs = 256 SIMDs each, one

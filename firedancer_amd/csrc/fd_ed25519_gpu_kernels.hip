@@ -334,15 +334,35 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
 #ifndef FD_FRONT_WAVES
 #define FD_FRONT_WAVES 1
 #endif
+#ifdef FD_FRONT_STAMPS
+/* diagnostic builds only (tools/front_stamps.py): histograms of the
+   front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
+   bins) for prep and decomp waves, accumulated over every launch with
+   vector atomics */
+__device__ unsigned long long fd_front_hist[2][256];
+extern "C" hipError_t fd_ed25519_gpu_front_hist( void * host, int clear ) {
+  if( clear ) { static unsigned long long z[2][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_front_hist), sizeof(fd_front_hist), 0, hipMemcpyDeviceToHost );
+}
+#endif
 extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
 fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
+#ifdef FD_FRONT_STAMPS
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if( blockIdx.x < nb_prep )
     fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, NULL );
   else
     fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
+#ifdef FD_FRONT_STAMPS
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;      /* 10 ns ticks */
+  unsigned b = (unsigned)(dt / 200ULL); if( b > 255u ) b = 255u;
+  if( (threadIdx.x & 63u) == 0u ) atomicAdd( &fd_front_hist[blockIdx.x < nb_prep ? 0 : 1][b], 1ULL );
+#endif
 }
 
 /* ------------------------------------------------------------------ */
