@@ -102,9 +102,9 @@ def parse():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--latency-batches", type=int, default=10000, help="C2 latency: >= 10^4 batches (SURVEY 8d)")
     ap.add_argument("--ring-depth", type=int, default=8, help="ring slots of the C2 streaming leg")
-    ap.add_argument("--ring-window", type=int, default=5,
+    ap.add_argument("--ring-window", type=int, default=6,
                     help="batches in flight on the C2 streaming leg (below the depth: free slots on the least "
-                         "loaded CU group; 5 of 8 keeps p99 under 1 ms, profiles/r02_ring_sweep_window.jsonl)")
+                         "loaded CU group; 6 of 8 keeps p99 under 1 ms, profiles/r02_ring_sweep_contiguous.jsonl)")
     ap.add_argument("--dry-cpu", action="store_true", help="rehearse the multi-rank plumbing on the CPU (tests only)")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
