@@ -208,10 +208,14 @@ int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 
 /* CU groups of the ring: slot s runs small batches (<= 64 signatures per
-   group CU) on the CUs c with c mod groups == s mod groups while another
-   ring batch is in flight, so concurrent small batches do not share SIMDs
-   (every group spans all XCDs).  Default min(depth, 4); 1 = none.  The
-   ring must be idle (nothing submitted or staged). */
+   group CU) on the contiguous logical-CU range
+   [g*ncu/groups, (g+1)*ncu/groups), g = s mod groups, while another ring
+   batch is in flight, so concurrent small batches do not share SIMDs.  On
+   MI355X each such range is a disjoint set of physical CUs spanning all 8
+   XCDs (tools/cu_mask_probe.hip, profiles/r02_cu_mask_probe.txt; an
+   interleaved c mod groups mask does NOT confine waves there).  Default
+   min(depth, 4); 1 = none.  The ring must be idle (nothing submitted or
+   staged). */
 int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * gpu, int groups );
 int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
 
