@@ -149,6 +149,8 @@ def lib() -> ctypes.CDLL:
         L.fd_vt_tcache_delete.restype = None
         L.fd_ed25519_gpu_debug_k.argtypes = [vp, ul, vp, ul, vp, vp, vp]
         L.fd_ed25519_gpu_debug_k.restype = ip
+        L.fd_ed25519_gpu_debug_fe.argtypes = [vp, ip, ul, vp, vp, vp]
+        L.fd_ed25519_gpu_debug_fe.restype = ip
         L.fd_ed25519_gpu_sha512_packed.argtypes = [vp, ul, vp, ul, vp, vp, ip]
         L.fd_ed25519_gpu_sha512_packed.restype = ip
         L.fd_ed25519_gpu_default.argtypes = []
@@ -350,6 +352,19 @@ class Engine:
         if err:
             raise EngineError(f"debug_k: {strerror(err)}: {last_error()}")
         return k, st
+
+    def debug_fe(self, op: int, f: np.ndarray, g: np.ndarray) -> np.ndarray:
+        """Diagnostics: the device field products (fd_k_debug_fe op 0-6) of
+        operand pairs f, g ([n,10] int32 limbs) -> [3,n,10] int32 limbs."""
+        f = np.ascontiguousarray(f, dtype=np.int32).reshape(-1, 10)
+        g = np.ascontiguousarray(g, dtype=np.int32).reshape(-1, 10)
+        if f.shape != g.shape:
+            raise EngineError("debug_fe: f and g differ in shape")
+        h = np.zeros((3, len(f), 10), np.int32)
+        err = lib().fd_ed25519_gpu_debug_fe(self._h, int(op), len(f), _p(f), _p(g), _p(h))
+        if err:
+            raise EngineError(f"debug_fe: {strerror(err)}: {last_error()}")
+        return h
 
     def sha512(self, msgs, is384: bool = False) -> list:
         """SHA-512 (SHA-384) digests of byte strings on the device."""

@@ -791,6 +791,35 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   return 1;
 }
 
+/* Diagnostics: the device field products (fd_k_debug_fe, ops 0-6) over n
+   operand pairs f, g ([n][10] int32 limbs); h receives [3][n][10] limbs.
+   Synchronous; host buffers; n <= 2^20. */
+extern "C" int fd_ed25519_gpu_debug_fe( fd_ed25519_gpu_t * g, int op, unsigned long n, int const * f, int const * gg, int * h ) {
+  if( !g || op < 0 || op > 6 || n > (1UL<<20) || (n && (!f || !gg || !h)) ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( g->lock );
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
+  if( !sl ) return FD_ED25519_ERR_ARG;
+  hipStream_t st = sl->stream;
+  unsigned long sz = 40UL * n;
+  int32_t * d = NULL;
+  int err = 0;
+  if( (e = hipMalloc( (void **)&d, 5UL * sz )) != hipSuccess ) return fd_gpu_fail( "debug_fe alloc", e );
+  if( (e = hipMemcpyAsync( d, f, sz, hipMemcpyHostToDevice, st )) != hipSuccess
+   || (e = hipMemcpyAsync( d + 10UL*n, gg, sz, hipMemcpyHostToDevice, st )) != hipSuccess
+   || (e = fd_ed25519_gpu_launch_debug_fe( op, n, d, d + 10UL*n, d + 20UL*n, st )) != hipSuccess
+   || (e = hipMemcpyAsync( h, d + 20UL*n, 3UL * sz, hipMemcpyDeviceToHost, st )) != hipSuccess
+   || (e = hipEventRecord( sl->done, st )) != hipSuccess ) { err = fd_gpu_fail( "debug_fe", e ); (void)hipStreamSynchronize( st ); }
+  else if( (err = fd_event_wait( sl->done, fd_timeout( g ) )) ) {
+    sl->ticket = g->next_ticket++; sl->orphan = 1;
+    return err;     /* the buffer may still be in use: leaked */
+  }
+  hipFree( d );
+  return err;
+}
+
 /* Diagnostics: k = SHA-512(R||A||M) mod L of each signature, computed by
    fd_k_prep on the device (the SURVEY.md section 7 minimum-slice check:
    compared with the reference's fd_sha512_* + fd_ed25519_sc_reduce,

@@ -1439,6 +1439,54 @@ extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * 
   return hipGetLastError();
 }
 
+/* diagnostics (fd_ed25519_gpu_debug_fe): the field products the kernels
+   are built from, as device code, one lane per operand pair (f, g as
+   [n][10] limbs; h as [3][n][10]), for a limb-for-limb comparison with the
+   reference's AVX field ops (avx/fd_ed25519_fe_avx_inl.h:484-677) on the
+   GPU itself -- tests/test_fe_host.py checks the same functions compiled
+   for the host, where the value barriers are empty.
+     0 fd_fe_mul            h0 = f g            (quad DSM, final, decomp)
+     1 fd_fe_sqn n=1        h0 = f^2            (decomp, pool doubling)
+     2 fd_fe_sqn n=2        h0 = 2 f^2
+     3 fd_fe_mul_ilp        h0 = f g            (independent column chains)
+     4 fd_fe_mul2           h0 = f g, h1 = g f  (uniform DSM, pool additions)
+     5 fd_fe_chain3         h0 = f g, h1 = g f, h2 = f f (pool p1p1 -> p2)
+     6 fd_fe_sqn2           h0 = f^2, h1 = 2 g^2 (pool doubling) */
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_debug_fe( int op, uint64_t n, int32_t const * __restrict__ f, int32_t const * __restrict__ g, int32_t * __restrict__ h ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  fe a, b, r0, r1, r2;
+#pragma unroll
+  for( int k=0; k<10; k++ ) { a.v[k] = f[i*10 + k]; b.v[k] = g[i*10 + k]; }
+  fd_fe_set( r0, 0 ); fd_fe_set( r1, 0 ); fd_fe_set( r2, 0 );
+  switch( op ) {
+  case 0: fd_fe_mul( r0, a, b ); break;
+  case 1: fd_fe_sqn( r0, a, 1 ); break;
+  case 2: fd_fe_sqn( r0, a, 2 ); break;
+  case 3: fd_fe_mul_ilp( r0, a, b ); break;
+  case 4: fd_fe_mul2( r0, a, b, r1, b, a ); break;
+  case 5: {
+    int32_t a2[10], a19[10], b2[10], b19[10];
+    fd_fe_pre_f( a2, a ); fd_fe_pre_g( a19, a ); fd_fe_pre_f( b2, b ); fd_fe_pre_g( b19, b );
+    fd_mul_cols c0 = { a.v, a2, b.v, b19 }, c1 = { b.v, b2, a.v, a19 }, c2 = { a.v, a2, a.v, a19 };
+    fd_fe_chain3( r0, r1, r2, c0, c1, c2 );
+    break;
+  }
+  case 6: fd_fe_sqn2( r0, a, 1, r1, b, 2 ); break;
+  default: break;
+  }
+#pragma unroll
+  for( int k=0; k<10; k++ ) { h[i*10 + k] = r0.v[k]; h[(n + i)*10 + k] = r1.v[k]; h[(2*n + i)*10 + k] = r2.v[k]; }
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch_debug_fe( int op, uint64_t n, int32_t const * f, int32_t const * g, int32_t * h,
+                                                     hipStream_t stream ) {
+  if( !n ) return hipSuccess;
+  hipLaunchKernelGGL( fd_k_debug_fe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, n, f, g, h );
+  return hipGetLastError();
+}
+
 extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                               fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
                                               uint64_t pool_min, uint64_t quad_max ) {

@@ -51,6 +51,8 @@ hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25
                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
 hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                          fd_ed25519_gpu_work_t const * w, uint64_t * kout, hipStream_t stream );
+hipError_t fd_ed25519_gpu_launch_debug_fe( int op, uint64_t n, int32_t const * f, int32_t const * g, int32_t * h,
+                                           hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                          void * out, int is384, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
