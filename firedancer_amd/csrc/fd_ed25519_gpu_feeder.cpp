@@ -240,6 +240,13 @@ FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed2551
   return 0;
 }
 
+/* Spins for up to FD_JOB_SPIN_NS before sleeping in short steps: a
+   4,096-signature batch completes every ~0.15 ms on a busy ring, and a
+   producer that sleeps between them pays a scheduler wake-up (tens of us
+   to ms on a shared host) before its next push -- after such a stall it
+   pushes its whole window at once and the batches convoy on the CU groups
+   (tools/ring_tail.py). */
+#define FD_JOB_SPIN_NS (1000000UL)
 FD_EXPORT int fd_ed25519_gpu_job_wait( fd_ed25519_gpu_job_t const * j, long timeout_ns ) {
   if( !j ) return FD_ED25519_ERR_ARG;
   unsigned long t0 = fd_feeder_now();
@@ -247,8 +254,9 @@ FD_EXPORT int fd_ed25519_gpu_job_wait( fd_ed25519_gpu_job_t const * j, long time
     int s = __atomic_load_n( &j->state, __ATOMIC_ACQUIRE );
     if( s == 1 ) return 0;
     if( s < 0 ) return s;
-    if( timeout_ns >= 0 && fd_feeder_now() - t0 > (unsigned long)timeout_ns ) return FD_ED25519_ERR_GPU;
-    if( it < 4096 ) __builtin_ia32_pause();
+    unsigned long dt = fd_feeder_now() - t0;
+    if( timeout_ns >= 0 && dt > (unsigned long)timeout_ns ) return FD_ED25519_ERR_GPU;
+    if( dt < FD_JOB_SPIN_NS ) __builtin_ia32_pause();
     else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
   }
 }
