@@ -113,7 +113,7 @@ static __device__ __forceinline__ void
 fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
               fd_ed25519_gpu_desc_t const * __restrict__ desc,
               int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-              uint8_t * sha_stage, uint64_t * __restrict__ kout ) {
+              uint8_t * sha_stage, uint64_t * __restrict__ kout, int sigmajor ) {
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
   /* a descriptor outside the blob is reported, never dereferenced (the
@@ -157,7 +157,12 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
   uint32_t kw[8];
 #pragma unroll
   for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
-  op_start[i] = fd_recode( sw, kw, ops + i, n );
+  /* op stream layout: step-major [t][n] for the uniform and pooled DSMs
+     (the slots a pool steps together sit at similar t, so one row's cache
+     line serves many of them); signature-major [n][FD_OPS_MAX] for the
+     quad DSM, which copies its 16 signatures' streams to LDS as 16-byte
+     rows (fd_quad_body) */
+  op_start[i] = sigmajor ? fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 ) : fd_recode( sw, kw, ops + i, n );
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4)
@@ -165,7 +170,7 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_e
            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
            uint64_t * __restrict__ kout ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
-  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, kout );
+  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, kout, 0 );
 }
 
 /* ------------------------------------------------------------------ */
@@ -354,7 +359,7 @@ fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if( blockIdx.x < nb_prep )
-    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, NULL );
+    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, NULL, 1 );
   else
     fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
 #ifdef FD_FRONT_STAMPS
@@ -659,9 +664,13 @@ FD_QDEV void fd_q_dblmix( fe & x, uint32_t m03, uint32_t s02 ) {
 }
 
 #define FD_QSIGS 16   /* signatures per 64-lane wave */
+/* a signature's op bytes in LDS: FD_OPS_MAX + 16 (132 dwords: the 16
+   rows start 4 banks apart, so the step's byte reads of 16 signatures at
+   one t hit 16 different banks; 16-byte aligned for ds_write_b128) */
+#define FD_QOPS_ROW (FD_OPS_MAX + 16)
 struct fd_quad_lds {
   int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
-  uint8_t ops[FD_OPS_MAX][FD_QSIGS];
+  uint8_t ops[FD_QSIGS][FD_QOPS_ROW];   /* signature-major, padded rows */
 };
 /* the two-waves-per-SIMD form: Ai lanes unpadded (40 B), nothing else in
    LDS (op bytes and Bi come from global memory, loaded a step ahead) --
@@ -732,13 +741,19 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
   }
 
-  /* op streams of the wave's 16 signatures -> LDS (rows from the wave's
-     first op on) */
+  /* op streams of the wave's 16 signatures (signature-major in HBM) ->
+     LDS as 16-byte pieces from the wave's first op on: at most 8
+     independent loads per lane (a byte per lane per load, as before, was a
+     ~100-deep chain of dependent round trips in front of the first step) */
   int t0 = fd_wave_min( start );
   if constexpr( !LITE ) {
-    for( int t=t0+(int)(lane>>4); t<FD_OPS_MAX; t+=4 ) {
-      uint64_t gs = sig0 + (lane & 15u);
-      L.ops[t][lane & 15u] = gs < n ? ops[(uint64_t)t*n + gs] : (uint8_t)0;
+    int const c0 = t0 >> 4;
+    for( int c=(int)lane; c<FD_QSIGS*(FD_OPS_MAX/16); c+=64 ) {
+      int sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
+      if( ch < c0 ) continue;
+      uint64_t gs = sig0 + (uint64_t)sg;
+      int4 v = gs < n ? *(int4 const *)(ops + gs*FD_OPS_MAX + (uint64_t)ch*16u) : make_int4( 0, 0, 0, 0 );
+      *(int4 *)&L.ops[sg][ch*16] = v;
     }
     for( int k=lane; k<8*FD_TAB_ENTRY; k+=64 ) L.tab[FD_QSIGS][k] = fd_gpu_bi_tab[k];
   }
@@ -783,15 +798,15 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
   /* LITE: this signature's op byte for the next step, loaded a step ahead */
-  uint8_t const * ops_i = ops + ii;
+  uint8_t const * ops_i = ops + ii*FD_OPS_MAX;   /* signature-major (fd_k_front) */
   int opn = 0;
-  if constexpr( LITE ) opn = (t0 >= start && t0 < FD_OPS_MAX) ? (int)ops_i[(uint64_t)t0*n] : 0;
+  if constexpr( LITE ) opn = (t0 >= start && t0 < FD_OPS_MAX) ? (int)ops_i[t0] : 0;
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
     int op;
     if constexpr( LITE ) {
       op = opn;
-      opn = (t + 1 >= start && t + 1 < FD_OPS_MAX) ? (int)ops_i[(uint64_t)(t + 1)*n] : 0;
-    } else op = t >= start ? (int)L.ops[t][ls] : 0;
+      opn = (t + 1 >= start && t + 1 < FD_OPS_MAX) ? (int)ops_i[t + 1] : 0;
+    } else op = t >= start ? (int)L.ops[ls][t] : 0;
     uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
     uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */

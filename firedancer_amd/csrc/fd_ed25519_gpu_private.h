@@ -7,7 +7,9 @@
 
 /* Per-batch HBM working set, SoA [field][item] (sizes for capacity N):
      status   int32 [N]          prep result (S check) or pending
-     ops      uint8 [512][N]     per-signature DSM op stream, right aligned
+     ops      uint8 [512][N]     per-signature DSM op stream, right aligned; step-major
+                                 for the uniform/pooled DSMs, [N][512] signature-major
+                                 for the quad DSM (fd_k_front writes it)
      op_start int32 [N]          first op index (FD_OPS_MAX if none)
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
