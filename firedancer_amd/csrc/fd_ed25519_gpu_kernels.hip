@@ -640,6 +640,8 @@ template<int CTRL> FD_QDEV void fd_fe_qperm( fe & o, fe const & x ) {
 #pragma unroll
   for( int k=0; k<10; k++ ) o.v[k] = fd_qperm<CTRL>( x.v[k] );
 }
+/* (x & m) ^ s as one v_bitop3_b32 (truth table of S0 & S1 ^ S2) */
+FD_QDEV uint32_t fd_andxor( uint32_t x, uint32_t m, uint32_t s ) { return __builtin_amdgcn_bitop3_b32( x, m, s, 0x6A ); }
 /* ((x & m) ^ s) - s: x, 0, -x or (m = 0, s = ~0) 0, for masks in {0, ~0} */
 FD_QDEV uint32_t fd_qterm( uint32_t x, uint32_t m, uint32_t s ) { return ((x & m) ^ s) - s; }
 
@@ -837,9 +839,13 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     fd_fe_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fe_qperm<FD_QP(2,2,2,2)>( w, C );
     uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
     uint32_t gs = (q==1u && !add) ? 1u : 0u;
+    /* u + fd_qterm( w, mW, mq2 ) as u + ((w & mW) ^ mq2) + (mq2 & 1): one
+       v_bitop3 and one v_add3 per limb (-s == s & 1 for a mask s; LLVM
+       otherwise selects between w & mW and its negation) */
+    uint32_t const s2b = (uint32_t)fd_opaque( (int32_t)(mq2 & 1u) );
 #pragma unroll
     for( int k=0; k<10; k++ ) {
-      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_qterm( (uint32_t)w.v[k], mW, mq2 ) );
+      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_andxor( (uint32_t)w.v[k], mW, mq2 ) + s2b );
       f.v[k] = (int32_t)fk;
       g.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
     }
