@@ -1227,17 +1227,26 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
       int tn = t + 1;
       int opn = tn < FD_OPS_MAX ? (int)ops[(uint64_t)tn*n + sg] : 0;   /* prefetch */
-      fe4 vt;
-      fd_pool_ld( vt, L, s );
-      if( kind ) fd_pool_add( vt, op, tab + sg*FD_TAB_ENTRY, n*FD_TAB_ENTRY, fd_gpu_bi_tab );
-      else       fd_pool_dbl( vt );
-      if( tn < FD_OPS_MAX ) {
+      /* load, step and store inside each op kind's branch: with the state
+         merged after the branch, LLVM gave the new and the old state the
+         same registers and copied the old limbs away first (~33 moves per
+         step) */
+      if( kind ) {
+        fe4 vt; fd_pool_ld( vt, L, s );
+        fd_pool_add( vt, op, tab + sg*FD_TAB_ENTRY, n*FD_TAB_ENTRY, fd_gpu_bi_tab );
         fd_pool_st( L, s, vt );
-        nm = (tn << 8) | opn;
       } else {
+        fe4 vt; fd_pool_ld( vt, L, s );
+        fd_pool_dbl( vt );
+        fd_pool_st( L, s, vt );
+      }
+      nm = tn < FD_OPS_MAX ? ((tn << 8) | opn) : EMPTY;
+      /* a stream that ended: its final p1p1 state out, from the slot (once
+         per signature, off the step's path) */
+      if( tn >= FD_OPS_MAX ) {
+        fe4 vf; fd_pool_ld( vf, L, s );
 #pragma unroll
-        for( int k=0; k<40; k++ ) fin[(uint64_t)k*m + sg] = vt.l[k/10].v[k%10];
-        nm = EMPTY;
+        for( int k=0; k<40; k++ ) fin[(uint64_t)k*m + sg] = vf.l[k/10].v[k%10];
       }
     }
     fd_mem_fence();
