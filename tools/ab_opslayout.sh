@@ -1,3 +1,7 @@
+# Experiment record (profiles/r02_quad_ops_sigmajor.txt): A/B of step-major vs signature-major op
+# streams for every DSM, with the since-removed FD_OPS_SIGMAJOR build switch (lib_tmajor.so =
+# -DFD_OPS_SIGMAJOR=0).  Kept for the record; the product now uses signature-major streams
+# for the quad DSM only.
 set -o pipefail
 mkdir -p gpurun_out
 N=firedancer_amd/libfd_ed25519_gpu.so; O=firedancer_amd/variants/lib_tmajor.so
