@@ -75,11 +75,17 @@ FD_DEV int fd_wn_step( fd_wn & v ) {
   uint32_t win = v.d[0] & 31u;
   int neg = win >= 16u;
   /* bits 0..4 hold win, so subtracting it never borrows; a negative digit
-     then adds 2^5 (carry propagated) */
-  uint64_t c = (uint64_t)(v.d[0] - win) + (neg ? 32u : 0u);
-  v.d[0] = (uint32_t)c;
+     then adds 2^5, which carries out of the low word only when its bits
+     5..31 are all set (a rare branch, so the common step is three
+     instructions instead of a 64-bit carry chain over all eight words) */
+  uint32_t d0 = v.d[0] - win;
+  uint32_t n0 = d0 + (neg ? 32u : 0u);
+  v.d[0] = n0;
+  if( __builtin_expect( n0 < d0, 0 ) ) {
+    uint64_t c = 1;
 #pragma unroll
-  for( int j=1; j<8; j++ ) { c = (uint64_t)v.d[j] + (c >> 32); v.d[j] = (uint32_t)c; }
+    for( int j=1; j<8; j++ ) { c += (uint64_t)v.d[j]; v.d[j] = (uint32_t)c; c >>= 32; }
+  }
   fd_wn_norm( v );
   return neg ? (int)win - 32 : (int)win;
 }
@@ -99,21 +105,25 @@ FD_DEV int fd_recode( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t 
      order: with cnt adds already placed (all at lower bits, or S's at
      the same bit), a digit at bit b goes to FD_OPS_MAX-1-(b+cnt).  At a
      shared bit S's digit is placed first (it is the later op). */
-  fd_wn vs, vk;
-  fd_wn_init( vs, sw );
-  fd_wn_init( vk, kw );
+  /* va is the scalar whose digit comes next (a_s: it is S); after each
+     digit the two swap if the other one's next digit is lower (or at the
+     same bit and the other is S), so the step runs in place */
+  fd_wn va, vb;
+  fd_wn_init( va, sw );
+  fd_wn_init( vb, kw );
+  int a_s = 1;
+  if( vb.pos < va.pos ) { fd_wn t = va; va = vb; vb = t; a_s = 0; }
   int cnt = 0;
   /* scalars below 2^253 have every digit at bit <= 253 and at most 2 x 127
-     of them; the bounds only keep a corrupted state inside the buffer */
-  while( (vs.pos != FD_WN_DONE || vk.pos != FD_WN_DONE) && cnt < 2*128 ) {
-    int take_s = vs.pos <= vk.pos;
-    fd_wn v = take_s ? vs : vk;
-    int b  = v.pos;
+     of them; the bounds only keep a corrupted state inside the buffer
+     (va.pos <= vb.pos, so va done means both are) */
+  while( va.pos != FD_WN_DONE && cnt < 2*128 ) {
+    int b  = va.pos;
     if( b > 255 ) break;
-    int dg = fd_wn_step( v );
-    ops[(uint64_t)(FD_OPS_MAX - 1 - (b + cnt))*stride] = fd_op_enc( take_s, dg );
+    int dg = fd_wn_step( va );
+    ops[(uint64_t)(FD_OPS_MAX - 1 - (b + cnt))*stride] = fd_op_enc( a_s, dg );
     cnt++;
-    if( take_s ) vs = v; else vk = v;
+    if( vb.pos < va.pos || (vb.pos == va.pos && !a_s) ) { fd_wn t = va; va = vb; vb = t; a_s ^= 1; }
   }
   return FD_OPS_MAX - 256 - cnt;
 }
