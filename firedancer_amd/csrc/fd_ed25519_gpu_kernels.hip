@@ -355,6 +355,9 @@ fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
+#ifdef FD_FRONT_PRIO
+  __builtin_amdgcn_s_setprio( FD_FRONT_PRIO );   /* experiment: issue ahead of co-resident quad-DSM waves */
+#endif
 #ifdef FD_FRONT_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
