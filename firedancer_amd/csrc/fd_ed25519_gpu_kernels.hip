@@ -162,7 +162,15 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
      line serves many of them); signature-major [n][FD_OPS_MAX] for the
      quad DSM, which copies its 16 signatures' streams to LDS as 16-byte
      rows (fd_quad_body) */
-  op_start[i] = sigmajor ? fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 ) : fd_recode( sw, kw, ops + i, n );
+  if( sigmajor ) {
+    /* the signature's own 512-byte row is zeroed here (the step-major
+       layout is zeroed by a memset before the launch; this one needs none,
+       so a small batch's front end is one launch) */
+    int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
+#pragma unroll
+    for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
+    op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
+  } else op_start[i] = fd_recode( sw, kw, ops + i, n );
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4)
@@ -1385,9 +1393,14 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
-  hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
-  if( e != hipSuccess ) return e;
   int quad = n < pool_min && !portable && n <= quad_max;
+  /* step-major op streams are zero-filled first; the quad schedule's
+     signature-major rows are zeroed by their own prep lanes (only rows of
+     signatures still pending after the S check are ever read) */
+  if( !quad ) {
+    hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+    if( e != hipSuccess ) return e;
+  }
   if( quad ) {
     /* latency path: prep and decomp in one launch (their time lands in phase 1) */
     unsigned const bt = 64u*FD_FRONT_WAVES;
