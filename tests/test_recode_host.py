@@ -35,7 +35,10 @@ def expected_stream(oracle, s, k):
 
 def edge_scalars():
     return [0, 1, 2, 15, 16, 17, 31, 32, L - 1, L - 2, 2**252, 2**252 - 1, 2**200, 2**64, 2**32 + 1,
-            (2**253 - 1) // 3, 2**253 - 1 - 2**130, int("10000" * 50, 2), int("11111" * 50, 2)]
+            (2**253 - 1) // 3, 2**253 - 1 - 2**130, int("10000" * 50, 2), int("11111" * 50, 2),
+            # a negative digit whose +2^5 carries out of the low word (and on
+            # through all-ones words): the recoder's rare carry branch
+            2**32 - 15, 2**64 - 15, 2**96 - 15, 2**224 - 15, (2**252 - 1) ^ 0x0e]
 
 
 def test_recode_vs_oracle_slide(harness, oracle):  # noqa: F811
