@@ -270,6 +270,24 @@ def test_pooled_equals_uniform(engine, pooled, n):
     engine.dsm_quad_max = 32768
 
 
+@pytest.mark.parametrize("sizes", [(40000, 4176, 40048, 4163)])
+def test_step_major_op_zeroing_vs_reference(pooled, uniform, ref, sizes):
+    """step-major op streams (pooled and uniform DSMs) are zero-filled
+    before fd_k_prep stores the additions; each batch runs on an op buffer
+    the previous, differently strided batch left full of additions (sizes
+    with and without a partly live last wave), and its codes must be the
+    reference's"""
+    base, _ = load_corpus("adversarial")
+    for eng in (pooled, uniform):
+        for n in sizes:
+            b = base.tile(int(np.ceil(n / len(base))))
+            b.desc = b.desc[:n]
+            got = eng.verify_packed(b.blob, b.desc)
+            exp = oracle_batch(ref, b)
+            bad = np.nonzero(got != exp)[0]
+            assert len(bad) == 0, (n, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]])
+
+
 @pytest.fixture(scope="module")
 def uniform():
     """an engine that runs the one-lane-per-signature DSM (fd_k_dsm) for
