@@ -710,6 +710,9 @@ template<int LITE> FD_QDEV void fd_q_tab_store_t( int32_t * p, fe const & v ) {
 #ifndef FD_QUAD_ILP
 #define FD_QUAD_ILP 0
 #endif
+#ifndef FD_QUAD_DPP_AND
+#define FD_QUAD_DPP_AND 1
+#endif
 /* products of the latency kernel.  FD_QUAD_ILP 1 = independent column
    chains (fd_fe_mul_ilp): measured equal (quad DSM 0.441 ms either way at
    4,096 signatures) -- a lone wave issues about one instruction per 4-5
@@ -873,6 +876,21 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     uint32_t mR = mq0 | mq1 | ~add, sR = mq0 | (mq3 & ~add);
     uint32_t mS = ~((mq0 | mq1) & add), sS = (mq0 & ~add) | (mq2 & ~pos) | (mq3 & pos);
     uint32_t cadd = (sR & 1u) + (sS & 1u);
+#if FD_QUAD_DPP_AND
+    /* each broadcast masked by a v_and_b32 with the quad move folded in
+       (VOP2 DPP); the barriers keep LLVM from fusing and + xor into a
+       v_bitop3 (VOP3, which takes no DPP operand on gfx950) */
+    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
+    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( h.v[k] ) & mPv) );
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( h.v[k] ) & mQv) );
+      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( h.v[k] ) & mRv) );
+      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( h.v[k] ) & mSv) );
+      vt.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + cadd);
+    }
+#else
     fe P, Q, R, S;
     fd_fe_qperm<FD_QP(0,0,0,0)>( P, h ); fd_fe_qperm<FD_QP(1,1,1,1)>( Q, h );
     fd_fe_qperm<FD_QP(2,2,2,2)>( R, h ); fd_fe_qperm<FD_QP(3,3,3,3)>( S, h );
@@ -880,6 +898,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     for( int k=0; k<10; k++ )
       vt.v[k] = (int32_t)(((uint32_t)P.v[k] & mP) + (((uint32_t)Q.v[k] & mQ) << qs)
                           + (((uint32_t)R.v[k] & mR) ^ sR) + (((uint32_t)S.v[k] & mS) ^ sS) + cadd);
+#endif
   }
 
   /* final p1p1 -> p2: q0 X = t0 t3, q1 Y = t1 t2, q2 Z = t2 t3; then
