@@ -19,6 +19,10 @@
 #ifndef FD_ED25519_GPU_FE_H
 #define FD_ED25519_GPU_FE_H
 
+#ifndef FD_FE_ADD_TWICE
+#define FD_FE_ADD_TWICE 1
+#endif
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -49,6 +53,19 @@ FD_DEV int64_t fd_opaque64( int64_t x ) {
   asm( "" : "+v"(x) );
 #endif
   return x;
+}
+
+/* 2x mod 2^32 as one v_add_u32 (full rate): LLVM selects v_lshlrev_b32
+   for both x*2 and x+x, which issues at half rate on gfx950
+   (profiles/r02_ubench_int.txt).  Not volatile: unused results drop out. */
+FD_DEV int32_t fd_twice( int32_t x ) {
+#if defined(__HIP_DEVICE_COMPILE__) && FD_FE_ADD_TWICE
+  int32_t r;
+  asm( "v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x) );
+  return r;
+#else
+  return fd_opaque( (int32_t)(2u*(uint32_t)x) );
+#endif
 }
 
 /* m ? a : b bitwise for a lane mask m in {0, ~0} (v_bfi_b32) */
@@ -327,7 +344,7 @@ struct fd_sq_cols {
    484-590): 2*f for odd limbs and 19*g, formed mod 2^32. */
 FD_DEV void fd_fe_pre_f( int32_t (&f2)[10], fd_gpu_fe_t const & f ) {
 #pragma unroll
-  for( int i=0; i<10; i++ ) f2[i] = (i&1) ? fd_opaque( (int32_t)(2u*(uint32_t)f.v[i]) ) : f.v[i];
+  for( int i=0; i<10; i++ ) f2[i] = (i&1) ? fd_twice( f.v[i] ) : f.v[i];
 }
 FD_DEV void fd_fe_pre_g( int32_t (&g19)[10], fd_gpu_fe_t const & g ) {
 #pragma unroll
@@ -400,7 +417,9 @@ struct fd_sq_ops {
 #pragma unroll
     for( int i=0; i<10; i++ ) {
       F[i]   = fe.v[i];
-      F2[i]  = fd_opaque( (int32_t)(2u *(uint32_t)fe.v[i]) );
+      /* each formed from F in one instruction (4F as 2(2F) or 38F as
+         2(19F) would need 2F or 19F for limbs that do not use them) */
+      F2[i]  = fd_twice( fe.v[i] );
       F4[i]  = fd_opaque( (int32_t)(4u *(uint32_t)fe.v[i]) );
       F19[i] = fd_opaque( (int32_t)(19u*(uint32_t)fe.v[i]) );
       F38[i] = fd_opaque( (int32_t)(38u*(uint32_t)fe.v[i]) );
