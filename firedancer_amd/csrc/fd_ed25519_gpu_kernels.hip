@@ -822,7 +822,13 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     if constexpr( LITE ) {
       op = opn;
       opn = (t + 1 >= start && t + 1 < FD_OPS_MAX) ? (int)ops_i[t + 1] : 0;
-    } else op = t >= start ? (int)L.ops[ls][t] : 0;
+    } else {
+      /* no t >= start guard: a pending signature's row is zero below its
+         op_start (its prep lane zeroed the whole row before recoding), and
+         any other row's bytes only steer lanes whose result is discarded
+         (code != FD_ST_PENDING), with table indices bounded by the masks */
+      op = (int)L.ops[ls][t];
+    }
     uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
     uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
