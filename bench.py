@@ -26,7 +26,6 @@ Extra measurements on rank 0 at N=1:
                sample of the same corpus, all host threads of this rank
 """
 import argparse
-import gc
 import json
 import math
 import os
@@ -437,6 +436,10 @@ def main():
             res["latency"]["lower_latency_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), 4)
             # one batch in flight at a time: the per-batch floor
             res["latency"]["depth1"] = ring_stream(fa, base, local, max(a.latency_batches // 5, 20), 1)
+            # open loop: batches offered at a fixed 40 M verifies/s (one per
+            # 102.4 us), at most the ring's depth outstanding
+            res["latency"]["paced_40M"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
+                                                      window=a.ring_depth, period_ns=int(BATCH_SIGS / 40e6 * 1e9))
             res["ring_4096_verifies_per_s"] = res["latency"]["pcie_inclusive_verifies_per_s"]
         if not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, usable_cores())
@@ -451,15 +454,17 @@ def main():
         dist.destroy_process_group()
 
 
-def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None):
+def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None, period_ns=0):
     """C2 at its own granularity: nb 4096-signature batches streamed through
     one engine's pinned ring by its per-GPU feeder thread
     (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
     ways included.  The corpus blob is registered with the engine (as a
     tile registers its input dcache), so a batch is DMA'd from where it
-    lies with no staging memcpy.  `window` batches are outstanding at any
-    time (default: the ring depth, so no batch waits in the feeder's
-    queue); latency = push -> codes on the host."""
+    lies with no staging memcpy.  The producer is the library's native
+    synthetic-load loop (fd_ed25519_gpu_feeder_synth, the counterpart of
+    the reference's synth-load verify tile): `window` batches outstanding
+    (closed loop), or one batch pushed every period_ns (paced, at most
+    `window` outstanding).  latency = push -> codes on the host."""
     eng = fa.Engine(device, max_sigs=BATCH_SIGS, max_blob=8 << 20, depth=depth)
     try:
         if groups:
@@ -470,57 +475,36 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
             eng.register(base.blob)
         feeder = fa.Feeder(eng)
         starts = np.random.default_rng(seed).integers(0, len(base) - BATCH_SIGS, 64)
-        descs = [np.ascontiguousarray(base.desc[s:s + BATCH_SIGS]) for s in starts]
         W = window or depth
-        jobs = [fa.Job() for _ in range(W)]
-        outs = [np.full(BATCH_SIGS, 99, np.int32) for _ in range(W)]
-        lat, qlat, hist = [], [], {"0": 0}
-
-        def done(k):
-            feeder.wait(jobs[k])
-            j = jobs[k]
-            lat.append((j.t_done_ns - j.t_push_ns) * 1e-6)
-            qlat.append((j.t_done_ns - j.t_submit_ns) * 1e-6)
-            # the producer stays light between pushes (a full histogram only
-            # when a batch holds a reject)
-            bad = np.count_nonzero(outs[k])
-            hist["0"] += BATCH_SIGS - bad
-            if bad:
-                for c, v in codes_hist(outs[k][outs[k] != 0]).items():
-                    hist[c] = hist.get(c, 0) + v
-
-        # no collector pauses in the producer loop: a full collection over the
-        # process's objects (torch, numpy, the corpus) stalls it for
-        # milliseconds, after which it pushes its whole window at once
-        gc_was = gc.isenabled()
-        gc.disable()
         t0 = time.perf_counter()
-        try:
-            for i in range(nb):
-                k = i % W
-                if i >= W:
-                    done(k)
-                feeder.push(base.blob, descs[i % len(descs)], outs[k], jobs[k])
-            for i in range(nb, nb + W):
-                if i - W < nb and i >= W:
-                    done(i % W)
-            wall = time.perf_counter() - t0
-        finally:
-            if gc_was:
-                gc.enable()
+        st = feeder.synth(base.blob, base.desc, BATCH_SIGS, starts, nb, W, period_ns)
+        wall = time.perf_counter() - t0
         numa = feeder.numa_node
         feeder.close()
-        lat = np.array(lat[W:]) if len(lat) > 2 * W else np.array(lat)
-        qlat = np.array(qlat[W:]) if len(qlat) > 2 * W else np.array(qlat)
-        return {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
-                "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "registered_source": bool(register),
-                "feeder_numa_node": numa,
-                "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
-                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
-                "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
-                "submit_to_done_p50_ms": float(np.percentile(qlat, 50)),
-                "submit_to_done_p99_ms": float(np.percentile(qlat, 99)),
-                "codes": hist, "codes_ok": valid_corpus_ok(hist, nb * BATCH_SIGS)}
+        skip = W if nb > 2 * W else 0          # the ring's fill
+        st = st[skip:]
+        lat = (st["t_done_ns"] - st["t_push_ns"]) * 1e-6
+        qlat = (st["t_done_ns"] - st["t_submit_ns"]) * 1e-6
+        hop = (st["t_submit_ns"] - st["t_push_ns"]) * 1e-6
+        c = st["codes"].sum(axis=0)
+        hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
+        res = {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
+               "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "registered_source": bool(register),
+               "feeder_numa_node": numa, "producer": "native (fd_ed25519_gpu_feeder_synth)",
+               "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
+               "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+               "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
+               "submit_to_done_p50_ms": float(np.percentile(qlat, 50)),
+               "submit_to_done_p99_ms": float(np.percentile(qlat, 99)),
+               "push_to_submit_p50_ms": float(np.percentile(hop, 50)),
+               "push_to_submit_p99_ms": float(np.percentile(hop, 99)),
+               "codes": hist, "codes_ok": valid_corpus_ok(hist, nb * BATCH_SIGS) and bool((st["state"] == 1).all())}
+        if period_ns:
+            sl = (st["t_done_ns"] - st["t_sched_ns"]) * 1e-6
+            res.update(offered_verifies_per_s=BATCH_SIGS / (period_ns * 1e-9),
+                       sched_to_done_p50_ms=float(np.percentile(sl, 50)),
+                       sched_to_done_p99_ms=float(np.percentile(sl, 99)))
+        return res
     finally:
         eng.close()
 

@@ -95,6 +95,10 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_public_batch.restype = None
         L.fd_ed25519_gpu_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fd_ed25519_gpu_submit.restype = ip
+        L.fd_ed25519_gpu_try_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fd_ed25519_gpu_try_submit.restype = ip
+        L.fd_ed25519_gpu_feeder_synth.argtypes = [vp, vp, ul, vp, ul, ul, vp, ul, ul, ip, ul, vp]
+        L.fd_ed25519_gpu_feeder_synth.restype = ip
         L.fd_ed25519_gpu_poll.argtypes = [vp, ul, vp, ip]
         L.fd_ed25519_gpu_poll.restype = ip
         L.fd_ed25519_gpu_depth.argtypes = [vp]
@@ -461,6 +465,11 @@ class Job(ctypes.Structure):
                 ("t_push_ns", ctypes.c_ulong), ("t_submit_ns", ctypes.c_ulong), ("t_done_ns", ctypes.c_ulong)]
 
 
+# fd_ed25519_gpu_synth_stat_t
+SYNTH_STAT_DTYPE = np.dtype([("t_sched_ns", "<u8"), ("t_push_ns", "<u8"), ("t_submit_ns", "<u8"), ("t_done_ns", "<u8"),
+                             ("state", "<i4"), ("codes", "<u4", (5,))], align=True)
+
+
 class Feeder:
     """The per-GPU feeder thread (fd_ed25519_gpu_feeder_t) over an Engine's ring."""
 
@@ -491,9 +500,30 @@ class Feeder:
 
     def wait(self, job: Job, timeout_ns: int = -1) -> None:
         err = lib().fd_ed25519_gpu_job_wait(ctypes.byref(job), timeout_ns)
-        self._keep.pop(ctypes.addressof(job), None)
+        # the arrays stay referenced until the job reached a final state: after
+        # a timeout it is still queued or in flight on the feeder thread, which
+        # may yet read the blob and descriptors and write the codes
+        # (close() releases them once the feeder has drained)
+        if job.state != 0:
+            self._keep.pop(ctypes.addressof(job), None)
         if err:
             raise EngineError(f"job: {strerror(err)}: {last_error()}")
+
+    def synth(self, blob: np.ndarray, desc: np.ndarray, batch_sigs: int, starts, nbatch: int, window: int,
+              period_ns: int = 0) -> np.ndarray:
+        """The native synthetic-load producer (fd_ed25519_gpu_feeder_synth): nbatch
+        jobs of batch_sigs signatures, job i from desc[starts[i % len(starts)]:],
+        closed loop with `window` outstanding (period_ns 0) or paced one job per
+        period_ns.  Returns the per-job SYNTH_STAT_DTYPE records."""
+        blob = np.ascontiguousarray(blob, np.uint8)
+        desc = np.ascontiguousarray(desc, DESC_DTYPE)
+        st = np.ascontiguousarray(starts, np.uint64)
+        stat = np.zeros(nbatch, SYNTH_STAT_DTYPE)
+        err = lib().fd_ed25519_gpu_feeder_synth(self._h, _p(blob), blob.nbytes, _p(desc), len(desc), batch_sigs,
+                                                _p(st), len(st), nbatch, window, period_ns, _p(stat))
+        if err:
+            raise EngineError(f"feeder synth: {strerror(err)}: {last_error()}")
+        return stat
 
     def close(self):
         if self._h:

@@ -38,6 +38,11 @@
 
 #define FD_EXPORT extern "C" __attribute__((visibility("default")))
 
+/* an idle feeder polls for new jobs this long before it sleeps */
+#ifndef FD_FEEDER_SPIN_NS
+#define FD_FEEDER_SPIN_NS (5000000UL)
+#endif
+
 static inline unsigned long fd_feeder_now( void ) {
   struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t );
   return (unsigned long)t.tv_sec * 1000000000UL + (unsigned long)t.tv_nsec;
@@ -54,6 +59,8 @@ struct fd_ed25519_gpu_feeder {
   std::mutex                           lock;
   std::condition_variable              cv;
   std::deque<fd_ed25519_gpu_job_t *>   queue;
+  std::atomic<unsigned long>           queued;      /* jobs pushed (the idle spin polls this, not the lock) */
+  std::atomic<int>                     sleeping;    /* the thread waits on cv: a push must notify */
   std::deque<fd_feeder_inflight>       inflight;
   std::vector<unsigned long>           zombies;     /* tickets of batches given up on (timed out): drained later */
   std::vector<fd_ed25519_gpu_desc_t>   rebased;
@@ -108,9 +115,9 @@ static int fd_feeder_submit( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t *
   fd_ed25519_gpu_desc_t * rd = f->rebased.data();
   fd_ed25519_desc_rebase( n, j->desc, j->blob_sz, b0, rd );
   unsigned long ticket = 0;
-  int err = fd_ed25519_gpu_submit( f->gpu, n, (uint8_t const *)j->blob + b0, b1 - b0, rd, &ticket );
-  if( err == FD_ED25519_ERR_ARG ) return 0;                       /* every slot in flight */
-  if( err ) { fd_job_finish( j, err ); return -1; }
+  int r = fd_ed25519_gpu_try_submit( f->gpu, n, (uint8_t const *)j->blob + b0, b1 - b0, rd, &ticket );
+  if( !r ) return 0;                                               /* every slot in flight */
+  if( r < 0 ) { fd_job_finish( j, r ); return -1; }               /* a real error ends the job */
   j->t_submit_ns = fd_feeder_now();
   f->inflight.push_back( fd_feeder_inflight{ j, ticket } );
   return 1;
@@ -193,10 +200,23 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
       __builtin_ia32_pause();
       continue;
     }
+    /* idle: spin on the push counter for FD_FEEDER_SPIN_NS after the last
+       progress before sleeping, so a producer that pushes the next batch
+       right after the previous one completes does not pay a scheduler
+       wake-up on this thread (tens of us to ms on a shared host: the
+       push -> submit tail of the C2 ring) */
+    if( fd_feeder_now() - last < FD_FEEDER_SPIN_NS && !f->halt.load() ) {
+      unsigned long q0 = f->queued.load( std::memory_order_acquire );
+      for( int k=0; k<64 && f->queued.load( std::memory_order_acquire ) == q0; k++ ) __builtin_ia32_pause();
+      continue;
+    }
     std::unique_lock<std::mutex> g( f->lock );
     if( f->queue.empty() && !pending ) {
       if( f->halt.load() ) break;
+      f->sleeping.store( 1 );
       f->cv.wait_for( g, std::chrono::milliseconds( 50 ) );
+      f->sleeping.store( 0 );
+      last = fd_feeder_now();
     }
   }
 }
@@ -206,6 +226,7 @@ FD_EXPORT fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_feeder_new( fd_ed25519_gpu_t 
   fd_ed25519_gpu_feeder_t * f = new fd_ed25519_gpu_feeder_t();
   f->gpu = gpu;
   f->halt.store( 0 );
+  f->queued.store( 0 ); f->sleeping.store( 0 );
   f->max_sigs = fd_ed25519_gpu_max_sigs( gpu );
   f->max_blob = fd_ed25519_gpu_max_blob( gpu );
   f->rebased.resize( f->max_sigs );
@@ -235,8 +256,9 @@ FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed2551
     std::lock_guard<std::mutex> g( f->lock );
     if( f->halt.load() ) return FD_ED25519_ERR_ARG;
     f->queue.push_back( j );
+    f->queued.fetch_add( 1, std::memory_order_release );
   }
-  f->cv.notify_one();
+  if( f->sleeping.load() ) f->cv.notify_one();
   return 0;
 }
 

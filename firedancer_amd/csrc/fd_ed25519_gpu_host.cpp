@@ -163,8 +163,8 @@ struct fd_ed25519_gpu {
   /* per-kernel HIP events of pipelined launches (fd_ed25519_gpu_dev_stats_*) */
   int           dev_stats_on;
   unsigned long dev_stats_cnt;
-  hipEvent_t    dev_ev[FD_DEV_STATS_MAX][FD_ED25519_GPU_KERNEL_CNT+1];
-  hipEvent_t    kev[FD_ED25519_GPU_KERNEL_CNT+1];   /* per-kernel timing events */
+  hipEvent_t    dev_ev[FD_DEV_STATS_MAX][FD_EV_CNT];
+  hipEvent_t    kev[FD_EV_CNT];   /* per-kernel timing events */
   std::mutex    lock;
 };
 
@@ -319,7 +319,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipEventCreateWithFlags( &g->dev_back[b],  hipEventDisableTiming ) );
     HIPCHK( hipEventRecord( g->dev_back[b], g->dev_sb ) );
   }
-  for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
+  for( int k=0; k<FD_EV_CNT; k++ ) HIPCHK( hipEventCreate( &g->kev[k] ) );
   return g;
 fail:
   fd_ed25519_gpu_delete( g );
@@ -367,7 +367,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
     if( sl->done   ) hipEventDestroy( sl->done );
   }
   for( int i=0; i<FD_DEV_STATS_MAX; i++ )
-    for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->dev_ev[i][k] ) hipEventDestroy( g->dev_ev[i][k] );
+    for( int k=0; k<FD_EV_CNT; k++ ) if( g->dev_ev[i][k] ) hipEventDestroy( g->dev_ev[i][k] );
   for( int b=0; b<2; b++ ) {
     if( g->dev_in[b]    ) hipEventDestroy( g->dev_in[b] );
     if( g->dev_front[b] ) hipEventDestroy( g->dev_front[b] );
@@ -376,7 +376,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   }
   if( g->dev_sf ) hipStreamDestroy( g->dev_sf );
   if( g->dev_sb ) hipStreamDestroy( g->dev_sb );
-  for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ ) if( g->kev[k] ) hipEventDestroy( g->kev[k] );
+  for( int k=0; k<FD_EV_CNT; k++ ) if( g->kev[k] ) hipEventDestroy( g->kev[k] );
   delete g;
 }
 
@@ -540,18 +540,17 @@ extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? 
    end overlaps launch k-1's DSM (its tail: the pool's last round of
    waves, ~0.9 ms per 1M-signature launch, tools/pool_rounds.py). */
 static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
-                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, int flags ) {
+                          fd_ed25519_gpu_desc_t const * d_desc, int * d_out, void * stream, int flags, fd_knobs const & kn ) {
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   int b = (int)(g->dev_seq & 1UL);
-  fd_knobs kn = fd_knobs_get( g );
   int mode = kn.mode | (kn.quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
   fd_ed25519_gpu_work_t const * w = &g->dev_work[b];
   hipEvent_t const * ev = NULL;
   if( g->dev_stats_on && g->dev_stats_cnt < FD_DEV_STATS_MAX ) {
     if( !g->dev_ev[g->dev_stats_cnt][0] )
-      for( int k=0; k<=FD_ED25519_GPU_KERNEL_CNT; k++ )
+      for( int k=0; k<FD_EV_CNT; k++ )
         if( (e = hipEventCreate( &g->dev_ev[g->dev_stats_cnt][k] )) != hipSuccess ) return fd_gpu_fail( "hipEventCreate", e );
     ev = g->dev_ev[g->dev_stats_cnt++];
   }
@@ -574,6 +573,12 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
    || (e = hipStreamWaitEvent( st, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (caller)", e );
   g->dev_seq++;
   return 0;
+}
+
+/* duration (ms) of kernel k of a launch timed with events ev[FD_EV_CNT]
+   (fd_ed25519_gpu_private.h: the DSM from the back part's own start) */
+static hipError_t fd_kernel_ms( float * ms, hipEvent_t const * ev, int k ) {
+  return hipEventElapsedTime( ms, ev[k == 3 ? FD_EV_BACK : k], ev[k+1] );
 }
 
 /* Per-kernel durations of the pipelined launches issued between begin
@@ -601,7 +606,7 @@ extern "C" int fd_ed25519_gpu_dev_stats_end( fd_ed25519_gpu_t * g, float * kerne
     if( err ) return err;
     for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) {
       float ms = 0.f;
-      if( (e = hipEventElapsedTime( &ms, g->dev_ev[i][k], g->dev_ev[i][k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
+      if( (e = fd_kernel_ms( &ms, g->dev_ev[i], k )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
       kernel_ms_sum[k] += ms;
     }
   }
@@ -628,8 +633,9 @@ extern "C" int fd_ed25519_gpu_verify_dev_ex( fd_ed25519_gpu_t * g, unsigned long
   if( !g || n > g->max_sigs || (n && (!d_blob || !d_desc || !d_out)) || (flags & ~FD_ED25519_GPU_DEV_INPUTS_READY) )
     return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
+  fd_knobs kn = fd_knobs_get( g );     /* before dev_lock: the engine's locks are never nested */
   std::lock_guard<std::mutex> guard( g->dev_lock );
-  return fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, flags );
+  return fd_dev_launch( g, n, d_blob, blob_sz, d_desc, d_out, stream, flags, kn );
 }
 
 extern "C" int fd_ed25519_gpu_verify_dev( fd_ed25519_gpu_t * g, unsigned long n, void const * d_blob, unsigned long blob_sz,
@@ -643,12 +649,12 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   if( !g || n > g->max_sigs || !kernel_ms || (n && (!d_blob || !d_desc || !d_out)) ) return FD_ED25519_ERR_ARG;
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ ) kernel_ms[k] = 0.f;
   if( !n ) return 0;
+  fd_knobs kn = fd_knobs_get( g );     /* before dev_lock: the engine's locks are never nested */
   std::lock_guard<std::mutex> guard( g->dev_lock );
   /* serial, on the caller's stream, so each kernel's events bracket it alone */
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e0 = hipSetDevice( g->device );
   if( e0 != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e0 );
-  fd_knobs kn = fd_knobs_get( g );
   int mode = kn.mode | (kn.quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0);
   if( (e0 = fd_dev_serial_begin( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   if( (e0 = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work[0], (int32_t *)d_out, st, g->kev,
@@ -658,7 +664,7 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], fd_timeout( g ) )) ) return err;
   hipError_t e;
   for( int k=0; k<FD_ED25519_GPU_KERNEL_CNT; k++ )
-    if( (e = hipEventElapsedTime( &kernel_ms[k], g->kev[k], g->kev[k+1] )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
+    if( (e = fd_kernel_ms( &kernel_ms[k], g->kev, k )) != hipSuccess ) return fd_gpu_fail( "elapsed", e );
   return 0;
 }
 
@@ -718,13 +724,20 @@ static int fd_ring_busy( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot const * sl ) 
 }
 
 /* On failure, whatever was already queued on the slot's stream (the H2D
-   copy from its pinned buffer, kernels on its scratch) is drained before
-   the slot can be picked again. */
+   copy from its pinned buffer, kernels on its scratch) must drain before
+   the slot can be picked again.  The drain is bounded by the engine's
+   timeout like every other wait; a stream that does not drain in time
+   leaves the slot orphaned (reclaimed by fd_free_slot once its event
+   completes) instead of blocking every user of the engine lock. */
 static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
                             unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
   hipStream_t st = NULL;
   int err = fd_slot_enqueue_( g, sl, n, blob, blob_sz, desc, &st );
-  if( err && st ) (void)hipStreamSynchronize( st );
+  if( err && st && fd_wait_query( fd_stream_query, (void *)st, FD_POLL_SPIN_NS, fd_timeout( g ) ) != 1 ) {
+    /* the slot's done event marks the end of what was queued on st */
+    if( hipEventRecord( sl->done, st ) == hipSuccess ) { sl->ticket = g->next_ticket++; sl->orphan = 1; }
+    else sl->ticket = ~0UL;   /* no event to wait on: never reused (leaked) */
+  }
   return err;
 }
 
@@ -753,20 +766,26 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   return 0;
 }
 
-extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
-                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                          fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
   if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
-  if( !sl ) return FD_ED25519_ERR_ARG;   /* ring full: poll first */
+  if( !sl ) return 0;                    /* ring full: poll first */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
   if( err ) return err;
   sl->staged = 0;
   sl->ticket = g->next_ticket++;
   *ticket = sl->ticket;
-  return 0;
+  return 1;
+}
+
+extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  int r = fd_ed25519_gpu_try_submit( g, n, blob, blob_sz, desc, ticket );
+  return r == 1 ? 0 : r == 0 ? FD_ED25519_ERR_ARG : r;
 }
 
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
@@ -832,8 +851,12 @@ extern "C" int fd_ed25519_gpu_debug_k( fd_ed25519_gpu_t * g, unsigned long n, vo
   if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!desc || !k_out || !status_out)) || (blob_sz && !blob) )
     return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
-  std::lock_guard<std::mutex> guard( g->lock );
+  /* the only place both engine locks are held: dev_lock first, as every
+     device-resident path takes it (none of them takes g->lock while
+     holding it: their knobs are read before), so no two threads can wait
+     on each other's lock */
   std::lock_guard<std::mutex> dguard( g->dev_lock );
+  std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );

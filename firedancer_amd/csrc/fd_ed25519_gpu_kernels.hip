@@ -1440,16 +1440,15 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
     hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
   }
   if( ev ) hipEventRecord( ev[2], stream );
-  if( n >= pool_min ) {
+  if( n >= pool_min )
     hipLaunchKernelGGL( fd_k_dsm_setup, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->tab, portable );
-    if( ev ) hipEventRecord( ev[3], stream );
-  }
+  if( ev ) hipEventRecord( ev[3], stream );   /* setup reads 0 on the other schedules */
   return hipGetLastError();
 }
 
 /* The back part: the DSM main loop and the compare (pooled: fd_k_dsm_pool
    + fd_k_dsm_final; latency: the quad DSM; between: the uniform DSM).
-   Timing events ev[3..5]. */
+   Timing events ev[FD_EV_BACK], ev[4], ev[5]. */
 extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                                   hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
@@ -1461,16 +1460,16 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
   int quad = n < pool_min && !portable && n <= quad_max;
   if( n >= pool_min ) {
     uint32_t nw = (uint32_t)((n + FD_POOL - 1) / FD_POOL);  /* one full pool per wave */
-    /* again on this stream: with the front part on another stream (the
-       pipelined device-resident path) the pool's events must both be on
-       the stream it runs on */
-    if( ev ) hipEventRecord( ev[3], stream );
+    /* the back part's own start event: with the front part on another
+       stream (the pipelined device-resident path) the pool's events must
+       both be on the stream it runs on */
+    if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
                         w->tab, w->pts, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
   } else if( quad ) {
-    if( ev ) hipEventRecord( ev[3], stream );
+    if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     if( flags & FD_ED25519_GPU_LAUNCH_QUAD2 )
       hipLaunchKernelGGL( fd_k_dsm_quad2, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
                           n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
@@ -1479,7 +1478,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
                           n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
     if( ev ) hipEventRecord( ev[4], stream );
   } else {
-    if( ev ) hipEventRecord( ev[3], stream );
+    if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     hipLaunchKernelGGL( fd_k_dsm,    dim3(nb),  dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
                         blob, desc, portable, strict );
     if( ev ) hipEventRecord( ev[4], stream );

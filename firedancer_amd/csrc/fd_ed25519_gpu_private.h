@@ -27,6 +27,14 @@ typedef struct fd_ed25519_gpu_work {
 /* bytes of HBM working set per signature of capacity */
 /* number of kernels in one launch (timed API) */
 #define FD_ED25519_GPU_KERNEL_CNT 5
+/* timing events of one launch: ev[k] .. ev[k+1] bracket kernel k on the
+   stream it runs on, except the DSM (kernel 3), which runs from the back
+   part's own start event ev[FD_EV_BACK] to ev[4]: in the pipelined
+   device-resident path the front part (ev[0..3]) and the back part run on
+   different streams, and a back-part event recorded into ev[3] would
+   overwrite the front's */
+#define FD_EV_BACK   (FD_ED25519_GPU_KERNEL_CNT+1)
+#define FD_EV_CNT    (FD_ED25519_GPU_KERNEL_CNT+2)
 
 /* op stream capacity: 256 doublings + at most 256 adds per scalar */
 #define FD_OPS_MAX 512

@@ -1,0 +1,112 @@
+/* fd_ed25519_gpu_synth.cpp -- synthetic load for the per-GPU feeder: the
+   producer side of a verify tile streaming fixed-size batches into one
+   engine's ring, as a native loop so the measured batch latency is the
+   engine's and not an interpreter's (a Python producer that stalls for a
+   collection or a GIL hand-off pushes its whole window at once and the
+   batches convoy on the CU groups).
+
+   The reference's counterpart is the synthetic-load verify tile
+   (src/app/frank/load/fd_frank_verify_synth_load.c:360-410), which
+   generates transactions, verifies each frag inline and stamps tsorig /
+   tspub per frag (:404-406); here each batch of batch_sigs signatures is
+   one feeder job and its push / submit / done stamps are kept.
+
+   Two arrival disciplines:
+     period_ns == 0  closed loop: `window` batches outstanding, the next
+                     pushed as soon as the oldest completes;
+     period_ns  > 0  paced: batch i is pushed at t0 + i*period_ns (offered
+                     load batch_sigs / period_ns), with at most `window`
+                     outstanding (a ring that cannot keep up is then
+                     closed-loop at the window, and its latency shows it).
+   Latency is push -> codes on the host (the job's t_done_ns - t_push_ns);
+   in paced mode late pushes are also reported from their scheduled time
+   (t_sched_ns) so a producer held back by a full window is not hidden. */
+
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "fd_ed25519_gpu.h"
+
+#define FD_EXPORT extern "C" __attribute__((visibility("default")))
+
+static inline unsigned long fd_synth_now( void ) {
+  struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t );
+  return (unsigned long)t.tv_sec * 1000000000UL + (unsigned long)t.tv_nsec;
+}
+
+/* busy-wait for a job (a tile polls its rings the same way), bounded */
+static int fd_synth_wait( fd_ed25519_gpu_job_t const * j, unsigned long bound_ns ) {
+  unsigned long t0 = fd_synth_now();
+  for(;;) {
+    int s = __atomic_load_n( &j->state, __ATOMIC_ACQUIRE );
+    if( s ) return s;
+    for( int k=0; k<32; k++ ) __builtin_ia32_pause();
+    if( fd_synth_now() - t0 > bound_ns ) return 0;
+  }
+}
+
+static void fd_synth_record( fd_ed25519_gpu_synth_stat_t * st, fd_ed25519_gpu_job_t const * j, unsigned long sched,
+                             int const * out ) {
+  st->t_sched_ns  = sched;
+  st->t_push_ns   = j->t_push_ns;
+  st->t_submit_ns = j->t_submit_ns;
+  st->t_done_ns   = j->t_done_ns;
+  st->state       = j->state;
+  for( int c=0; c<5; c++ ) st->codes[c] = 0;
+  if( j->state != 1 ) return;
+  for( unsigned long i=0; i<j->n; i++ ) {
+    int c = out[i];
+    st->codes[ c == 0 ? 0 : c == FD_ED25519_ERR_SIG ? 1 : c == FD_ED25519_ERR_PUBKEY ? 2 : c == FD_ED25519_ERR_MSG ? 3 : 4 ]++;
+  }
+}
+
+FD_EXPORT int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     f,
+                                           void const *                  blob,
+                                           unsigned long                 blob_sz,
+                                           fd_ed25519_gpu_desc_t const * desc,
+                                           unsigned long                 desc_cnt,
+                                           unsigned long                 batch_sigs,
+                                           unsigned long const *         starts,
+                                           unsigned long                 start_cnt,
+                                           unsigned long                 nbatch,
+                                           int                           window,
+                                           unsigned long                 period_ns,
+                                           fd_ed25519_gpu_synth_stat_t * stat ) {
+  if( !f || !blob || !desc || !starts || !start_cnt || !stat || !batch_sigs || window < 1 || window > 64 ) return FD_ED25519_ERR_ARG;
+  for( unsigned long k=0; k<start_cnt; k++ ) if( starts[k] > desc_cnt || desc_cnt - starts[k] < batch_sigs ) return FD_ED25519_ERR_ARG;
+  fd_ed25519_gpu_job_t * jobs  = (fd_ed25519_gpu_job_t *)calloc( (size_t)window, sizeof(fd_ed25519_gpu_job_t) );
+  int *                  outs  = (int *)malloc( (size_t)window * batch_sigs * sizeof(int) );
+  unsigned long *        sched = (unsigned long *)calloc( (size_t)window, sizeof(unsigned long) );
+  if( !jobs || !outs || !sched ) { free( jobs ); free( outs ); free( sched ); return FD_ED25519_ERR_GPU; }
+  unsigned long const bound = 30000000000UL;   /* 30 s per batch: a wedged device ends the run */
+  int err = 0;
+  unsigned long t0 = fd_synth_now();
+  unsigned long i = 0;
+  for( ; i<nbatch + (unsigned long)window && !err; i++ ) {
+    unsigned long k = i % (unsigned long)window;
+    if( i >= (unsigned long)window ) {
+      fd_ed25519_gpu_job_t * j = &jobs[k];
+      if( !fd_synth_wait( j, bound ) ) { err = FD_ED25519_ERR_GPU; break; }
+      fd_synth_record( &stat[i - (unsigned long)window], j, sched[k], outs + k*batch_sigs );
+      if( j->state < 0 ) err = j->state;
+    }
+    if( i >= nbatch ) continue;
+    unsigned long when = period_ns ? t0 + i*period_ns : 0UL;
+    if( period_ns ) while( fd_synth_now() < when ) __builtin_ia32_pause();
+    fd_ed25519_gpu_job_t * j = &jobs[k];
+    memset( j, 0, sizeof(*j) );
+    j->n = batch_sigs; j->blob = blob; j->blob_sz = blob_sz;
+    j->desc = desc + starts[i % start_cnt]; j->out = outs + k*batch_sigs;
+    sched[k] = period_ns ? when : 0UL;
+    int r = fd_ed25519_gpu_feeder_push( f, j );
+    if( r ) { err = r; break; }
+  }
+  if( err ) {
+    /* drain what is still outstanding before the buffers go away (each
+       wait bounded; a job never finished leaks its buffers) */
+    for( unsigned long k=0; k<(unsigned long)window; k++ )
+      if( jobs[k].n && !fd_synth_wait( &jobs[k], bound ) ) return err;
+  }
+  free( jobs ); free( outs ); free( sched );
+  return err;
+}

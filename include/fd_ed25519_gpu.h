@@ -198,6 +198,19 @@ fd_ed25519_gpu_submit( fd_ed25519_gpu_t *            gpu,
                        fd_ed25519_gpu_desc_t const * desc,
                        unsigned long *               ticket );
 
+/* As fd_ed25519_gpu_submit, but a full ring is not an error: returns 1
+   submitted (*ticket set), 0 no free slot (poll first), < 0 the batch
+   could not be run (FD_ED25519_ERR_ARG: bad arguments; FD_ED25519_ERR_GPU).
+   The per-GPU feeder submits through this, so a real argument error ends
+   its job instead of being retried as "ring full". */
+int
+fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t *            gpu,
+                           unsigned long                 n,
+                           void const *                  blob,
+                           unsigned long                 blob_sz,
+                           fd_ed25519_gpu_desc_t const * desc,
+                           unsigned long *               ticket );
+
 int
 fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
                      unsigned long      ticket,
@@ -387,6 +400,38 @@ int  fd_ed25519_gpu_feeder_push     ( fd_ed25519_gpu_feeder_t * feeder, fd_ed255
 /* Wait for a job: 0 done, its error code, or FD_ED25519_ERR_GPU after
    timeout_ns (< 0: no bound). */
 int  fd_ed25519_gpu_job_wait        ( fd_ed25519_gpu_job_t const * job, long timeout_ns );
+
+/* Synthetic load (the producer side of a verify tile, as the reference's
+   synthetic-load tile src/app/frank/load/fd_frank_verify_synth_load.c:
+   360-410): nbatch jobs of batch_sigs signatures each, job i taking the
+   descriptors desc[starts[i % start_cnt] .. + batch_sigs) into blob,
+   pushed to the feeder from a native loop on the calling thread.
+   period_ns == 0: closed loop, `window` (1..64) jobs outstanding;
+   period_ns > 0: job i pushed at t0 + i*period_ns (offered load
+   batch_sigs / period_ns), at most `window` outstanding.  stat[i] gets job
+   i's stamps (t_sched_ns = its scheduled push time in paced mode, else 0),
+   final state and a histogram of its codes: [0] SUCCESS, [1] ERR_SIG,
+   [2] ERR_PUBKEY, [3] ERR_MSG, [4] other.  Returns 0, FD_ED25519_ERR_ARG,
+   or the first job error (FD_ED25519_ERR_GPU if a job did not complete
+   within 30 s). */
+typedef struct fd_ed25519_gpu_synth_stat {
+  unsigned long t_sched_ns, t_push_ns, t_submit_ns, t_done_ns;
+  int           state;
+  unsigned int  codes[5];
+} fd_ed25519_gpu_synth_stat_t;
+
+int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     feeder,
+                                 void const *                  blob,
+                                 unsigned long                 blob_sz,
+                                 fd_ed25519_gpu_desc_t const * desc,
+                                 unsigned long                 desc_cnt,
+                                 unsigned long                 batch_sigs,
+                                 unsigned long const *         starts,
+                                 unsigned long                 start_cnt,
+                                 unsigned long                 nbatch,
+                                 int                           window,
+                                 unsigned long                 period_ns,
+                                 fd_ed25519_gpu_synth_stat_t * stat );
 
 /* ---- Multi-device --------------------------------
 

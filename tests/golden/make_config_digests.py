@@ -16,6 +16,11 @@ shipped; where it is, the tests also compare code by code.
          corrupted over all 18 invalid cases                      (C3 at C2 shape)
   c4     one 256-byte / 442-byte message, n = 1..16 and 4096 signers,
          25 % of the signatures corrupted (signature/key cases only)  (C4)
+  c3_10m the north star's 10M-signature adversarial corpus at C2 shape:
+         10 chunks of 1,000,000 txn signatures (seeds 4200+k), 10 %
+         corrupted over all 18 invalid cases, plus the three SURVEY Q2
+         vectors after chunk 0 -- 10,000,003 signatures; a digest per
+         chunk and the histogram of the whole                     (C3)
 
 Runs only in the build container (needs the reference build)."""
 import ctypes
@@ -58,6 +63,31 @@ def c3c2_batch(nthreads=8):
     return corpus.adversarial_txns(C3C2["n"], seed=C3C2["seed"], invalid_frac=C3C2["invalid_frac"], nthreads=nthreads)
 
 
+C3_10M = {"chunks": 10, "chunk": 1_000_000, "seed0": 4200, "invalid_frac": 0.1}
+# the three SURVEY.md section 8c Q2 vectors (msg, sig, pub hex): valid
+# signatures the reference rejects through its limb compare
+Q2_VECTORS = [
+    ("562c7b301299d47deefe44c5368b77333c214b79b3e7dc03b091f0add168c0910740ac7544423faa742c3ba3d5286c624e1c5174ae4ccad097bea9f3c3cc197f33b0c640b71ae479e30fb2b7159bfb099c9780aa80fff0c1ea9682838b906f8677ea561bef530df8f714bea2b6eeb81b7b468ab64220d9d62a00a557e66bb35d",
+     "a53f00568d07e4944ee86da222b258beae6d8353024faf57de1fa83b05eea496267f66788337eab61e0d36da454c46700ad217fb3cb08d3d016548e4ff5be803",
+     "5bba42a60de96030d8f6a85dc5809e3f39a210671f50ee0ffdab810e18725a49"),
+    ("b594272285085ae80737ae28cf824783a8788d96d301ef3376d5f6de6599498fe92ab86784c593a3d42802cb97dcd15797351268f765787d68e4b6053cef065acc426921518d814afde0ca82fd788941a87e9468af2070c05755a2caeb6bdd34b8d108fe1ae96d59f8017eb0fe18c1a6da300403730cc3344d8cf5ecdba1bce9",
+     "588e6a12357767161aae6b35a7768481883861dcb399c0929ba2319214871d93895b3ab2404066f4e92dba7c688dbca7874ef5c16bedcb1efc6eb50560fe3602",
+     "a8c5f0b9a0cad87801e0e550c7b4cda39c96cc31b6de89123437e41c3f42ccfe"),
+    ("fc2f6a47b996987a34e02bc58cc0e2f84144f1fa4a07d2964f2695e7daecdf8c1bb177623f9fe1d12b12a087383fa17153234d17507d1d45b5e009f968528efd7e51c1781977306ae975fee54e1665da6896fc2d53ce9ea9340282bbae55102db2dbaffb5798b0874037889b445e8b00afeeb1ad12f53e389f5cd7bc238bd4c9",
+     "f064a139d45ec0994e332d79364ddd8c2894a3a9b97b571e864efe0cf2fbae0055b9ce729e97564fe0bf3444b29719f1908388a5ff1807355cff0a69561fb003",
+     "1935951cae485585719b256b1132ccbc729da20b718cfe2950c18dcdd82bbd71")]
+
+
+def c3_10m_chunk(k, nthreads=8):
+    """chunk k of the 10M C3 corpus (chunk 0 carries the three Q2 vectors at its end)"""
+    b = corpus.adversarial_txns(C3_10M["chunk"], seed=C3_10M["seed0"] + k, invalid_frac=C3_10M["invalid_frac"],
+                                nthreads=nthreads)
+    if k == 0:
+        q = corpus.from_triples([(bytes.fromhex(m), bytes.fromhex(s), bytes.fromhex(p)) for m, s, p in Q2_VECTORS])
+        b = corpus.concat([b, q])
+    return b
+
+
 def c4_batch(msg_sz, n, nthreads=8):
     """(batch, shared msg, sig[n,64], pub[n,32]) for one C4 case"""
     b, msg, _, _ = corpus.single_msg(n, msg_sz, seed=5000 + 100 * n + msg_sz, nthreads=nthreads)
@@ -74,10 +104,31 @@ def ref_codes(L, b, threads=8):
     return out
 
 
+def c3_10m(L, nthreads=8):
+    chunks, tot, labels = [], {}, {}
+    for k in range(C3_10M["chunks"]):
+        b = c3_10m_chunk(k, nthreads)
+        e = ref_codes(L, b, nthreads)
+        chunks.append(digest(e))
+        for a, c in hist(e).items():
+            tot[a] = tot.get(a, 0) + c
+        for a, c in hist(b.label).items():
+            labels[a] = labels.get(a, 0) + c
+        print(f"c3_10m chunk {k}: {len(b)} sigs {hist(e)}", flush=True)
+    return dict(C3_10M, signatures=sum(tot.values()), chunk_digests=chunks, hist=tot, label_hist=labels)
+
+
 def main():
     # (the product library is only the signer here; importing this module
     # from the GPU tests must not change how the library loads)
     L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libfdref.so"))
+    if sys.argv[1:] == ["--only", "c3_10m"]:
+        path = os.path.join(HERE, "config_digests.json")
+        res = json.load(open(path))
+        res["c3_10m"] = c3_10m(L, os.cpu_count() or 8)
+        json.dump(res, open(path, "w"), indent=1)
+        print(json.dumps(res["c3_10m"]["hist"]))
+        return
     res = {"generator": "tests/golden/make_config_digests.py", "checker": "oracle/_ref/libfdref.so (reference AVX2 build)"}
     b = c1_batch()
     e = ref_codes(L, b)
@@ -94,6 +145,7 @@ def main():
             e = ref_codes(L, b)
             c4[f"{sz}/{n}"] = {"codes": e.tolist()} if n <= 16 else {"digest": digest(e), "hist": hist(e)}
     res["c4"] = {"sizes": list(C4_SIZES), "ns": C4_NS, "cases": C4_CASES, "expected": c4}
+    res["c3_10m"] = c3_10m(L)
     json.dump(res, open(os.path.join(HERE, "config_digests.json"), "w"), indent=1)
     print(json.dumps({k: v.get("hist") for k, v in res.items() if isinstance(v, dict) and "hist" in v}))
 

@@ -23,7 +23,7 @@ extern "C" int oracle_verify( void const * msg, unsigned long sz, void const * s
 #define FAKE_DEPTH_MAX 8
 struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket; int staged, polls, wedged; };
 struct fd_ed25519_gpu {
-  unsigned long max_sigs, max_blob, next; int depth, wedge; long timeout_ns;
+  unsigned long max_sigs, max_blob, next; int depth, wedge, fail_submit; long timeout_ns;
   fake_slot slot[ FAKE_DEPTH_MAX ];
   std::mutex lock;
 };
@@ -52,6 +52,8 @@ extern "C" int  fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { (void)g; r
 extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? __atomic_load_n( &g->timeout_ns, __ATOMIC_RELAXED ) : -1; }
 extern "C" int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long ns ) { if( !g ) return FD_ED25519_ERR_ARG; __atomic_store_n( &g->timeout_ns, ns, __ATOMIC_RELAXED ); return 0; }
 extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on ) { std::lock_guard<std::mutex> l( g->lock ); g->wedge = on; }
+/* the next try_submit fails with `code` (a runtime error on a free slot) */
+extern "C" void fake_engine_fail_submit( fd_ed25519_gpu_t * g, int code ) { std::lock_guard<std::mutex> l( g->lock ); g->fail_submit = code; }
 /* the HIP calls of the feeder (C linkage, as hip_runtime_api.h declares them) */
 extern "C" int hipDeviceGetPCIBusId( char * bus, int len, int device ) { (void)bus; (void)len; (void)device; return 1; }
 extern "C" int hipSetDevice( int device ) { (void)device; return 0; }
@@ -70,14 +72,15 @@ extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob 
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].blob == blob ) g->slot[s].staged = 0;
 }
 
-extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
-                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                          fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
   if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> l( g->lock );
   fake_slot * sl = NULL;
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && g->slot[s].blob == blob ) sl = &g->slot[s];
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) sl = &g->slot[s];
-  if( !sl ) return FD_ED25519_ERR_ARG;
+  if( !sl ) return 0;
+  if( g->fail_submit ) { int c = g->fail_submit; g->fail_submit = 0; return c; }
   if( sl->blob != blob ) memcpy( sl->blob, blob, blob_sz );
   if( sl->desc != desc ) memcpy( sl->desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   for( unsigned long i=0; i<n; i++ ) {
@@ -89,7 +92,12 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
   sl->n = n; sl->staged = 0; sl->polls = 0; sl->wedged = g->wedge;
   sl->ticket = g->next++;
   *ticket = sl->ticket;
-  return 0;
+  return 1;
+}
+extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                      fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  int r = fd_ed25519_gpu_try_submit( g, n, blob, blob_sz, desc, ticket );
+  return r == 1 ? 0 : r == 0 ? FD_ED25519_ERR_ARG : r;
 }
 
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {

@@ -2,7 +2,8 @@
    (firedancer_amd/csrc/fd_ed25519_gpu_feeder.cpp, unmodified) over the CPU
    fake engine, built with ASan/UBSan and separately with TSan.
 
-   1. two producer threads push 150 jobs each (random sizes, random
+   1. (1b: the native synthetic-load producer over the same feeder)
+      two producer threads push 150 jobs each (random sizes, random
       descriptors into one shared blob, ~2 % of them outside it); every
       job's codes must equal the restatement's verdict on the ORIGINAL
       descriptors (ERR_ARG for the bad ones): catches a misrouted batch, a
@@ -11,7 +12,10 @@
       ERR_GPU once the engine's timeout passes, a later job still runs on
       the slot that is left, and with every slot held by a batch given up
       on a queued job fails with ERR_GPU instead of waiting forever;
-   3. fd_ed25519_gpu_feeder_delete returns with given-up batches still on
+   3. a submit that fails with a real error (not "ring full") ends that
+      job with the error, under an UNBOUNDED engine timeout -- it is not
+      retried forever -- and the next job runs;
+   4. fd_ed25519_gpu_feeder_delete returns with given-up batches still on
       the device.
    Exit 0 and "ok" on success. */
 #include <stdio.h>
@@ -24,6 +28,7 @@
 
 extern "C" int  oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
 extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on );
+extern "C" void fake_engine_fail_submit( fd_ed25519_gpu_t * g, int code );
 
 #define CHECK( c ) do { if( !(c) ) { fprintf( stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c ); exit( 1 ); } } while( 0 )
 #define CHECK_EQ( a, b ) do { long a_ = (long)(a), b_ = (long)(b); if( a_ != b_ ) { fprintf( stderr, "FAIL %s:%d: %s = %ld, expected %ld\n", __FILE__, __LINE__, #a, a_, b_ ); exit( 1 ); } } while( 0 )
@@ -97,6 +102,58 @@ int main( void ) {
     sigs += jb.job.n;
   }
 
+  /* 1b. the native synthetic-load producer (fd_ed25519_gpu_synth.cpp),
+     closed loop and paced: every batch's code histogram equals the
+     restatement's over its descriptors, and the stamps are ordered */
+  {
+    unsigned long const BS = 64, NB = 40;
+    std::vector<fd_ed25519_gpu_desc_t> all( ITEMS );
+    std::vector<int> ref( ITEMS );
+    unsigned long s1 = 5;
+    for( unsigned long it=0; it<ITEMS; it++ ) {
+      fd_ed25519_gpu_desc_t d;
+      d.sig_off = (uint32_t)(it*ITEM_SZ); d.pub_off = (uint32_t)(it*ITEM_SZ + 64); d.msg_off = (uint32_t)(it*ITEM_SZ + 96);
+      d.msg_sz = (uint32_t)(rnd( &s1 ) % 129);
+      all[it] = d;
+      ref[it] = oracle_verify( blob.data() + d.msg_off, d.msg_sz, blob.data() + d.sig_off, blob.data() + d.pub_off );
+    }
+    unsigned long starts[5] = { 0, 100, 700, 1500, ITEMS - BS };
+    for( int mode=0; mode<2; mode++ ) {
+      std::vector<fd_ed25519_gpu_synth_stat_t> st( NB );
+      CHECK_EQ( fd_ed25519_gpu_feeder_synth( f, blob.data(), blob_sz, all.data(), ITEMS, BS, starts, 5, NB, 3,
+                                             mode ? 200000UL : 0UL, st.data() ), 0 );
+      for( unsigned long b=0; b<NB; b++ ) {
+        unsigned long h[5] = { 0, 0, 0, 0, 0 };
+        for( unsigned long i=0; i<BS; i++ ) {
+          int c = ref[starts[b % 5] + i];
+          h[ c == 0 ? 0 : c == -1 ? 1 : c == -2 ? 2 : c == -3 ? 3 : 4 ]++;
+        }
+        CHECK_EQ( st[b].state, 1 );
+        for( int c=0; c<5; c++ ) CHECK_EQ( st[b].codes[c], h[c] );
+        CHECK( st[b].t_push_ns <= st[b].t_submit_ns && st[b].t_submit_ns <= st[b].t_done_ns );
+        if( mode ) CHECK( st[b].t_sched_ns && st[b].t_sched_ns <= st[b].t_push_ns );
+      }
+    }
+    unsigned long bad_start[1] = { ITEMS };   /* a window past the descriptors */
+    std::vector<fd_ed25519_gpu_synth_stat_t> st( 1 );
+    CHECK_EQ( fd_ed25519_gpu_feeder_synth( f, blob.data(), blob_sz, all.data(), ITEMS, BS, bad_start, 1, 1, 1, 0UL, st.data() ), FD_ED25519_ERR_ARG );
+  }
+
+  /* 3 (before the wedge uses up the slots). a real submit error ends its
+     job, with no engine timeout to rescue a retry loop */
+  {
+    fd_ed25519_gpu_set_timeout( g, -1L );
+    unsigned long s3 = 99;
+    job_buf e, ok;
+    make_job( &e, blob.data(), blob_sz, &s3 ); make_job( &ok, blob.data(), blob_sz, &s3 );
+    fake_engine_fail_submit( g, FD_ED25519_ERR_GPU );
+    CHECK( fd_ed25519_gpu_feeder_push( f, &e.job ) == 0 );
+    CHECK_EQ( fd_ed25519_gpu_job_wait( &e.job, 5000000000L ), FD_ED25519_ERR_GPU );
+    CHECK( fd_ed25519_gpu_feeder_push( f, &ok.job ) == 0 );
+    CHECK_EQ( fd_ed25519_gpu_job_wait( &ok.job, 5000000000L ), 0 );
+    CHECK( ok.out == ok.exp );
+  }
+
   /* 2. a wedged device (the fake engine verifies inside submit, slowly
      under the sanitizers, so the short timeout is only set here) */
   fd_ed25519_gpu_set_timeout( g, 200000000L );                  /* 0.2 s */
@@ -114,7 +171,7 @@ int main( void ) {
   for( int k=0; k<2; k++ ) { make_job( &b[k], blob.data(), blob_sz, &s ); CHECK( fd_ed25519_gpu_feeder_push( f, &b[k].job ) == 0 ); }
   for( int k=0; k<2; k++ ) CHECK_EQ( fd_ed25519_gpu_job_wait( &b[k].job, 5000000000L ), FD_ED25519_ERR_GPU );   /* no slot left */
 
-  /* 3. delete with every slot held by a batch given up on */
+  /* 4. delete with every slot held by a batch given up on */
   fd_ed25519_gpu_feeder_delete( f );
   fd_ed25519_gpu_delete( g );
   printf( "ok %lu signatures in %d jobs\n", sigs, 2 * PER );

@@ -92,3 +92,29 @@ def test_bounded_wait_selftest():
     assert L.fd_ed25519_gpu_wait_selftest(2_000_000_000, 40_000_000) == 1  # ready after 40 ms (past the spin)
     assert L.fd_ed25519_gpu_wait_selftest(2_000_000_000, 0) == 1
     assert L.fd_ed25519_gpu_wait_selftest(1_000_000, 500_000_000) == 0   # late: timed out first
+
+
+def test_feeder_wait_keeps_arrays_until_final_state():
+    """Feeder.wait: a wait that times out leaves the job queued
+    or in flight on the feeder thread, so the blob, descriptors and out
+    array it references must stay alive; they are released only once the
+    job's state is final.  Driven through the real fd_ed25519_gpu_job_wait
+    on a job no feeder ever completes (no device needed)."""
+    f = fa.Feeder.__new__(fa.Feeder)
+    f._h, f._keep = None, {}
+    j = fa.Job()
+    j.state = 0
+    arrays = (np.zeros(8, np.uint8), np.zeros(1, fa.DESC_DTYPE), np.zeros(1, np.int32))
+    f._keep[ctypes.addressof(j)] = arrays
+    with pytest.raises(fa.EngineError):
+        f.wait(j, 2_000_000)                  # 2 ms: times out, job still pending
+    assert f._keep[ctypes.addressof(j)] is arrays
+    j.state = 1                               # the feeder finished it
+    f.wait(j, 2_000_000)
+    assert ctypes.addressof(j) not in f._keep
+    j2 = fa.Job()
+    j2.state = fa.ERR_GPU                     # a failed job is final too
+    f._keep[ctypes.addressof(j2)] = arrays
+    with pytest.raises(fa.EngineError):
+        f.wait(j2, 0)
+    assert ctypes.addressof(j2) not in f._keep

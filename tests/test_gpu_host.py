@@ -1,0 +1,118 @@
+"""Host-runtime behaviour on the GPU (round 3):
+
+  - the engine's two locks are never taken in opposite orders: the
+    diagnostic k path (debug_k) and device-resident launches (verify_dev)
+    from two threads at once finish (debug_k took g->lock then
+    dev_lock while verify_dev held dev_lock and read the knobs under
+    g->lock);
+  - the live per-kernel timing of pipelined launches attributes the DSM
+    setup and the pool to their own streams' events (the back
+    part re-recorded the front's ev[3]);
+  - the native synthetic-load producer (fd_ed25519_gpu_feeder_synth, the
+    bench's C2 ring driver) returns every batch's codes, closed loop and
+    paced, equal to the reference's."""
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import firedancer_amd as fa
+from conftest import oracle_batch
+from firedancer_amd import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def test_debug_k_and_verify_dev_concurrently(ref):
+    b = corpus.solana_txns(8192, seed=31)
+    exp = oracle_batch(ref, b)
+    e = fa.Engine(0, 1 << 14, 1 << 24)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
+    d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+    d_out = torch.zeros(len(b), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    errs, done = [], [0, 0]
+    stop = time.time() + 8.0
+
+    def launches():
+        try:
+            st = torch.cuda.Stream(dev)
+            while time.time() < stop:
+                e.verify_dev(len(b), d_blob.data_ptr(), len(b.blob), d_desc.data_ptr(), d_out.data_ptr(), st.cuda_stream)
+                st.synchronize()
+                assert (d_out.cpu().numpy() == exp).all()
+                done[0] += 1
+        except Exception as x:     # noqa: BLE001
+            errs.append(x)
+
+    def ks():
+        try:
+            while time.time() < stop:
+                k, st = e.debug_k(b.blob[:1 << 20], b.desc[:256])
+                assert (st != 0).any()
+                done[1] += 1
+        except Exception as x:     # noqa: BLE001
+            errs.append(x)
+
+    th = [threading.Thread(target=launches, daemon=True), threading.Thread(target=ks, daemon=True)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60.0)
+    assert not any(t.is_alive() for t in th), "engine locks deadlocked"
+    assert not errs, errs
+    assert done[0] > 3 and done[1] > 3, done
+    e.close()
+
+
+def test_pipelined_stats_attribute_setup_and_pool():
+    n = 1 << 18
+    b = corpus.solana_txns(n, seed=32)
+    e = fa.Engine(0, n, 1 << 29)
+    e.dsm_pool_min = 0                     # the pooled schedule: setup on the front stream, pool on the DSM stream
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
+    d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+    d_out = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    serial = e.verify_dev_timed(n, d_blob.data_ptr(), len(b.blob), d_desc.data_ptr(), d_out.data_ptr(), st)
+    e.dev_stats_begin()
+    for _ in range(6):
+        e.verify_dev(n, d_blob.data_ptr(), len(b.blob), d_desc.data_ptr(), d_out.data_ptr(), st, inputs_ready=True)
+    torch.cuda.synchronize()
+    live, launches = e.dev_stats_end()       # per-kernel mean ms over the launches
+    assert launches == 6
+    names = dict(zip(fa.Engine.KERNELS, range(5)))
+    setup, pool = live[names["fd_k_dsm_setup"]], live[names["fd_k_dsm_pool"]]
+    # setup is timed between its own front-stream events: it cannot absorb a
+    # wait for the previous launch's pool (which would make it pool-sized)
+    assert 0 < setup < 0.5 * pool, (live, serial)
+    # the pool, from the back part's own start event, is the pool alone
+    assert 0.7 * serial[names["fd_k_dsm_pool"]] < pool < 1.6 * serial[names["fd_k_dsm_pool"]], (live, serial)
+    assert (live >= 0).all()
+    e.close()
+
+
+@pytest.mark.parametrize("period_ns", [0, 150_000])
+def test_synth_producer_codes(ref, period_ns):
+    base = corpus.adversarial_txns(20000, seed=33, invalid_frac=0.1)
+    exp = oracle_batch(ref, base)
+    e = fa.Engine(0, 4096, 8 << 20, depth=8)
+    e.register(base.blob)
+    f = fa.Feeder(e)
+    starts = np.random.default_rng(3).integers(0, len(base) - 4096, 16)
+    st = f.synth(base.blob, base.desc, 4096, starts, 48, 6, period_ns)
+    f.close()
+    e.close()
+    assert (st["state"] == 1).all()
+    for i in range(48):
+        seg = exp[starts[i % 16]:starts[i % 16] + 4096]
+        want = [int((seg == 0).sum()), int((seg == -1).sum()), int((seg == -2).sum()), int((seg == -3).sum()), 0]
+        assert st["codes"][i].tolist() == want, i
+    assert (st["t_push_ns"] <= st["t_submit_ns"]).all() and (st["t_submit_ns"] <= st["t_done_ns"]).all()
+    if period_ns:
+        assert (np.diff(st["t_sched_ns"].astype(np.int64)) == period_ns).all()

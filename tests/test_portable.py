@@ -9,6 +9,7 @@ the reference's portable build compiled in place
 MODE_PORTABLE is checked against both."""
 import ctypes
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -26,7 +27,12 @@ Q2 = ("562c7b301299d47deefe44c5368b77333c214b79b3e7dc03b091f0add168c0910740ac754
 def refp():
     path = os.path.join(ROOT, "oracle", "_ref", "libfdref_portable.so")
     if not os.path.exists(path):
-        pytest.skip("reference portable build not available")
+        if os.path.isdir("/root/reference"):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True, capture_output=True)
+        else:
+            # shipped with the tree like libfdref.so: row f4's parity check
+            # never silently weakens to a skip
+            pytest.fail(f"{path} missing: build it in the container with make -C oracle ref")
     return ctypes.CDLL(path)
 
 
