@@ -454,7 +454,8 @@ def main():
         dist.destroy_process_group()
 
 
-def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None, period_ns=0):
+def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None, period_ns=0,
+                lat_dsm=None):
     """C2 at its own granularity: nb 4096-signature batches streamed through
     one engine's pinned ring by its per-GPU feeder thread
     (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
@@ -471,6 +472,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
             eng.cu_groups = groups
         if quad2 is not None:
             eng.quad2 = quad2
+        if lat_dsm is not None:
+            eng.lat_dsm = lat_dsm
         if register:
             eng.register(base.blob)
         feeder = fa.Feeder(eng)
@@ -489,7 +492,7 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         c = st["codes"].sum(axis=0)
         hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
         res = {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
-               "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "registered_source": bool(register),
+               "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "lat_dsm": eng.lat_dsm, "registered_source": bool(register),
                "feeder_numa_node": numa, "producer": "native (fd_ed25519_gpu_feeder_synth)",
                "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
