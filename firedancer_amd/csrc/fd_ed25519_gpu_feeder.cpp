@@ -272,7 +272,7 @@ FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed2551
 FD_EXPORT int fd_ed25519_gpu_job_wait( fd_ed25519_gpu_job_t const * j, long timeout_ns ) {
   if( !j ) return FD_ED25519_ERR_ARG;
   unsigned long t0 = fd_feeder_now();
-  for( unsigned long it=0;; it++ ) {
+  for(;;) {
     int s = __atomic_load_n( &j->state, __ATOMIC_ACQUIRE );
     if( s == 1 ) return 0;
     if( s < 0 ) return s;

@@ -3,7 +3,9 @@
    reference behaviour: src/app/frank/load/fd_frank_verify_synth_load.c:
    360-410, frag format src/disco/quic/fd_quic_tile.c:475-516).
 
-   Data flow per frag (host, single thread, as the reference tile):
+   Data flow per frag (host, single thread, as the reference tile; the
+   multi-engine feeder mode below differs only in where batches live and
+   how they reach the device):
      trailer -> fd_txn_t (signature / signer / message offsets)
      tag = first 8 bytes of signature 0 -> tcache; dup -> HA_FILT
      frag bytes -> the open batch's pinned staging blob (zero-copy submit:
@@ -103,10 +105,14 @@ struct fd_vt_txn {
 };
 
 struct fd_vt_batch {
-  uint8_t *               blob;   /* engine slot's pinned staging buffers */
+  uint8_t *               blob;   /* engine slot's pinned staging buffers (feeder mode: this batch's host buffers) */
   fd_ed25519_gpu_desc_t * desc;
   unsigned long           used, nsig, ticket;
   std::vector<fd_vt_txn>  txns;
+  /* feeder mode */
+  int                     eng;    /* engine (and feeder) the batch belongs to */
+  int *                   codes;
+  fd_ed25519_gpu_job_t    job;
 };
 
 struct fd_verify_tile {
@@ -120,6 +126,17 @@ struct fd_verify_tile {
   std::vector<fd_vt_batch *> pool;
   std::vector<int>          out;
   unsigned long             diag[ FD_VERIFY_TILE_DIAG_CNT ];
+  /* feeder mode (fd_verify_tile_new_multi): batches are built in host
+     buffers owned per engine (registered with it, so its feeder DMAs them
+     in place) and pushed round robin to the engines' feeders */
+  int                       multi, gpu_cnt, next;
+  fd_ed25519_gpu_t *        gpus   [ FD_VERIFY_TILE_GPU_MAX ];
+  fd_ed25519_gpu_feeder_t * feeders[ FD_VERIFY_TILE_GPU_MAX ];
+  uint8_t *                 region [ FD_VERIFY_TILE_GPU_MAX ];   /* one allocation per engine */
+  int                       reg_ok [ FD_VERIFY_TILE_GPU_MAX ];
+  unsigned long             region_sz;
+  std::vector<fd_vt_batch *> epool [ FD_VERIFY_TILE_GPU_MAX ];   /* free batches per engine */
+  std::vector<fd_vt_batch *> all;
 };
 
 static unsigned long fd_vt_now( void ) {
@@ -128,12 +145,27 @@ static unsigned long fd_vt_now( void ) {
 }
 
 static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
-  int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), block );
-  if( r <= 0 ) return r ? FD_ED25519_ERR_GPU : 0;
+  int const * codes;
+  if( t->multi ) {
+    /* the feeder finishes the job (state 1) or fails it (< 0); a blocking
+       wait is bounded by the engine's timeout */
+    int st = __atomic_load_n( &b->job.state, __ATOMIC_ACQUIRE );
+    if( !st && block ) {
+      int r = fd_ed25519_gpu_job_wait( &b->job, fd_ed25519_gpu_timeout( t->gpus[ b->eng ] ) );
+      st = r ? r : 1;
+    }
+    if( !st ) return 0;
+    if( st < 0 ) return FD_ED25519_ERR_GPU;
+    codes = b->codes;
+  } else {
+    int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), block );
+    if( r <= 0 ) return r ? FD_ED25519_ERR_GPU : 0;
+    codes = t->out.data();
+  }
   unsigned long tspub = fd_vt_now();
   for( fd_vt_txn const & x : b->txns ) {
     int ok = 1;
-    for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( t->out[ x.sig0 + k ] == FD_ED25519_SUCCESS );
+    for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( codes[ x.sig0 + k ] == FD_ED25519_SUCCESS );
     if( ok ) {
       if( t->publish ) t->publish( t->ctx, x.tag, b->blob + x.blob_off, x.sz, x.ctl, x.tsorig, tspub );
       t->diag[ FD_VERIFY_TILE_DIAG_PUB_CNT ]++;
@@ -144,7 +176,8 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
     }
   }
   b->txns.clear(); b->ticket = 0;
-  t->pool.push_back( b );
+  if( t->multi ) t->epool[ b->eng ].push_back( b );
+  else           t->pool.push_back( b );
   return 1;
 }
 
@@ -163,8 +196,15 @@ static int fd_vt_drain( fd_verify_tile_t * t, int block ) {
 static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
   if( !b || !b->nsig ) return 0;
-  int err = fd_ed25519_gpu_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
-  if( err ) return FD_ED25519_ERR_GPU;
+  if( t->multi ) {
+    memset( &b->job, 0, sizeof(b->job) );
+    b->job.n = b->nsig; b->job.blob = b->blob; b->job.blob_sz = b->used; b->job.desc = b->desc; b->job.out = b->codes;
+    if( fd_ed25519_gpu_feeder_push( t->feeders[ b->eng ], &b->job ) ) return FD_ED25519_ERR_GPU;
+    t->next = (b->eng + 1) % t->gpu_cnt;   /* the next batch goes to the next engine */
+  } else {
+    int err = fd_ed25519_gpu_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+    if( err ) return FD_ED25519_ERR_GPU;
+  }
   t->diag[ FD_VERIFY_TILE_DIAG_BATCH_CNT ]++;
   t->inflight.push_back( b );
   t->open = NULL;
@@ -178,14 +218,27 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
     if( err ) return err;
   }
   while( !t->open ) {
-    void * blob; fd_ed25519_gpu_desc_t * desc;
-    if( !fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ) {
-      fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
-      b->blob = (uint8_t *)blob; b->desc = desc; b->used = 0; b->nsig = 0; b->ticket = 0;
-      t->open = b;
-      break;
+    if( t->multi ) {
+      /* a free batch of the next engine in round-robin order */
+      for( int k=0; k<t->gpu_cnt && !t->open; k++ ) {
+        int e = (t->next + k) % t->gpu_cnt;
+        if( t->epool[e].empty() ) continue;
+        fd_vt_batch * b = t->epool[e].back(); t->epool[e].pop_back();
+        b->used = 0; b->nsig = 0; b->ticket = 0;
+        t->open = b;
+      }
+      if( t->open ) break;
+    } else {
+      void * blob; fd_ed25519_gpu_desc_t * desc;
+      if( !fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ) {
+        fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
+        b->blob = (uint8_t *)blob; b->desc = desc; b->used = 0; b->nsig = 0; b->ticket = 0;
+        t->open = b;
+        break;
+      }
     }
-    /* every ring slot busy: back-pressure until the oldest batch lands */
+    /* every ring slot (feeder mode: every batch buffer) busy: back-pressure
+       until the oldest batch lands */
     if( t->inflight.empty() ) return FD_ED25519_ERR_GPU;
     t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
     int err = fd_vt_drain( t, 1 );
@@ -216,8 +269,82 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
   return t;
 }
 
+/* Feeder mode: one tile driving gpu_cnt engines through their per-GPU
+   feeders (fd_ed25519_gpu_feeder_*: a thread per engine, pinned to the
+   GPU's NUMA node, keeping that engine's whole ring in flight).  Each
+   engine owns 2 x depth batch buffers in one host allocation registered
+   with it; batches go to the engines round robin and are published in
+   arrival order, as with one engine. */
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
+                                                       fd_verify_tile_cfg_t const * cfg,
+                                                       fd_verify_tile_publish_fn publish, void * ctx ) {
+  if( !gpus || !gpu_cnt || gpu_cnt > FD_VERIFY_TILE_GPU_MAX ) return NULL;
+  for( unsigned long e=0; e<gpu_cnt; e++ ) if( !gpus[e] ) return NULL;
+  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL };
+  if( cfg ) c = *cfg;
+  unsigned long maxs = ~0UL, maxb = ~0UL;
+  for( unsigned long e=0; e<gpu_cnt; e++ ) {
+    unsigned long s = fd_ed25519_gpu_max_sigs( gpus[e] ), b = fd_ed25519_gpu_max_blob( gpus[e] );
+    if( s < maxs ) maxs = s;
+    if( b < maxb ) maxb = b;
+  }
+  if( !c.batch_sigs || c.batch_sigs > maxs ) c.batch_sigs = maxs;
+  if( c.batch_sigs < FD_TXN_SIG_MAX ) return NULL;
+  fd_vt_tcache_t * tc = fd_vt_tcache_new( c.tcache_depth, c.tcache_map_cnt );
+  if( !tc ) return NULL;
+  fd_verify_tile_t * t = new fd_verify_tile_t();
+  t->gpu = gpus[0]; t->publish = publish; t->ctx = ctx; t->tc = tc;
+  t->batch_sigs = c.batch_sigs; t->max_blob = maxb; t->open = NULL;
+  t->multi = 1; t->gpu_cnt = (int)gpu_cnt; t->next = 0;
+  memset( t->diag, 0, sizeof(t->diag) );
+  /* per batch: blob (+64 pad, 64-aligned), descriptors, codes */
+  unsigned long blob_room = (maxb + 64UL + 63UL) & ~63UL;
+  unsigned long per = blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL)
+                    + ((c.batch_sigs * sizeof(int) + 63UL) & ~63UL);
+  int ok = 1;
+  for( unsigned long e=0; e<gpu_cnt && ok; e++ ) {
+    t->gpus[e] = gpus[e];
+    int nb = 2 * fd_ed25519_gpu_depth( gpus[e] );
+    t->region_sz = per * (unsigned long)nb;
+    void * r = NULL;
+    if( posix_memalign( &r, 4096UL, t->region_sz ) ) { ok = 0; break; }
+    t->region[e] = (uint8_t *)r;
+    memset( r, 0, t->region_sz );
+    /* registered: the feeder DMAs each batch in place (no staging copy);
+       without it (no GPU-visible mapping) the feeder copies it into a slot */
+    t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], r, t->region_sz );
+    for( int k=0; k<nb; k++ ) {
+      fd_vt_batch * b = new fd_vt_batch();
+      uint8_t * p = t->region[e] + per * (unsigned long)k;
+      b->blob  = p;
+      b->desc  = (fd_ed25519_gpu_desc_t *)(p + blob_room);
+      b->codes = (int *)(p + blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL));
+      b->eng = (int)e; b->ticket = 0; b->used = 0; b->nsig = 0;
+      t->epool[e].push_back( b );
+      t->all.push_back( b );
+    }
+    t->feeders[e] = fd_ed25519_gpu_feeder_new( gpus[e], 1 );
+    if( !t->feeders[e] ) ok = 0;
+  }
+  if( !ok ) { fd_verify_tile_delete( t ); return NULL; }
+  return t;
+}
+
 FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
   if( !t ) return;
+  if( t->multi ) {
+    /* feeder delete drains: every pushed job is finished (or failed after
+       the engine's timeout) before the buffers go away */
+    for( int e=0; e<t->gpu_cnt; e++ ) if( t->feeders[e] ) fd_ed25519_gpu_feeder_delete( t->feeders[e] );
+    for( int e=0; e<t->gpu_cnt; e++ ) {
+      if( t->region[e] && t->reg_ok[e] ) fd_ed25519_gpu_unregister( t->gpus[e], t->region[e] );
+      free( t->region[e] );
+    }
+    for( fd_vt_batch * b : t->all ) delete b;
+    fd_vt_tcache_delete( t->tc );
+    delete t;
+    return;
+  }
   while( !t->inflight.empty() ) {   /* results discarded, but the slots must drain */
     fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
     fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
@@ -288,6 +415,27 @@ FD_EXPORT int fd_verify_tile_rx_burst( fd_verify_tile_t * t, uint8_t const * bas
     if( err ) return err;
   }
   return 0;
+}
+
+FD_EXPORT int fd_verify_tile_rx_burst_now( fd_verify_tile_t * t, uint8_t const * base, uint64_t const * off,
+                                           uint32_t const * sz, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    int err = fd_verify_tile_rx( t, base + off[i], sz[i], i, fd_vt_now() );
+    if( err ) return err;
+  }
+  return 0;
+}
+
+FD_EXPORT void fd_verify_tile_lat_publish( void * ctx, unsigned long sig, void const * frag, unsigned long sz,
+                                           unsigned long ctl, unsigned long tsorig, unsigned long tspub ) {
+  (void)sig; (void)frag; (void)sz; (void)ctl;
+  fd_verify_tile_lat_t * h = (fd_verify_tile_lat_t *)ctx;
+  unsigned long d = tspub >= tsorig ? tspub - tsorig : 0UL;
+  unsigned long b = d / 1000UL;
+  if( b >= FD_VERIFY_TILE_LAT_BINS ) { b = FD_VERIFY_TILE_LAT_BINS - 1UL; h->over++; }
+  h->bin[ b ]++;
+  h->cnt++; h->sum_ns += d;
+  if( d > h->max_ns ) h->max_ns = d;
 }
 
 FD_EXPORT int fd_verify_tile_service( fd_verify_tile_t * t, int flush ) {

@@ -15,7 +15,10 @@
        backpressure (:185-194): no credits -> IN_BACKP = 1, BACKP_CNT++;
        the frag path: next frag from the input -> fd_verify_tile_rx
          (HA dedup, staging into the pinned ring, batch submit).
-   fini: drains and frees (the reference's tile process simply exits). */
+   fini: drains and frees (the reference's tile process simply exits).
+   device_cnt > 1: one engine per device and the tile in feeder mode
+   (fd_verify_tile_new_multi), so one tile process can drive every GPU of
+   the node whatever verify_tile_count is. */
 
 #include <linux/unistd.h>
 #include <string.h>
@@ -65,8 +68,22 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
   a->close_fd_start    = 4U;   /* stdin, stdout, stderr, logfile (fd_frank_verify.c:16) */
   a->allow_syscalls_sz = (unsigned short)(sizeof(fd_vt_allow_syscalls) / sizeof(fd_vt_allow_syscalls[0]));
   a->allow_syscalls    = fd_vt_allow_syscalls;
-  a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, a->depth ? a->depth : 3 );
-  a->tile = a->gpu ? fd_verify_tile_new( a->gpu, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+  int depth = a->depth ? a->depth : 3;
+  if( a->device_cnt > 1 ) {
+    /* one engine per device, the tile in feeder mode */
+    int cnt = a->device_cnt > FD_VERIFY_TILE_GPU_MAX ? FD_VERIFY_TILE_GPU_MAX : a->device_cnt;
+    int ndev = fd_ed25519_gpu_device_cnt();
+    int ok = ndev > 0;
+    for( int e=0; e<cnt && ok; e++ ) {
+      a->gpus[e] = fd_ed25519_gpu_new_ex( (a->device + e) % ndev, a->max_sigs, a->max_blob, depth );
+      ok = a->gpus[e] != NULL;
+    }
+    a->gpu  = a->gpus[0];
+    a->tile = ok ? fd_verify_tile_new_multi( a->gpus, (unsigned long)cnt, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+  } else {
+    a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, depth );
+    a->tile = a->gpu ? fd_verify_tile_new( a->gpu, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+  }
   if( !a->gpu || !a->tile ) {
     a->err = FD_ED25519_ERR_GPU;
     if( a->cnc ) fd_vt_cnc_set( a->cnc, FD_VERIFY_TILE_SIGNAL_FAIL );
@@ -139,7 +156,10 @@ static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
 
 static void fd_vt_task_fini( fd_verify_tile_args_t * a ) {
   fd_verify_tile_delete( a->tile ); a->tile = NULL;
-  fd_ed25519_gpu_delete( a->gpu );  a->gpu  = NULL;
+  if( a->device_cnt > 1 ) {
+    for( int e=0; e<FD_VERIFY_TILE_GPU_MAX; e++ ) { fd_ed25519_gpu_delete( a->gpus[e] ); a->gpus[e] = NULL; }
+  } else fd_ed25519_gpu_delete( a->gpu );
+  a->gpu = NULL;
 }
 
 FD_EXPORT fd_verify_tile_task_t fd_verify_tile_task = {

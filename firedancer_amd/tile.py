@@ -38,17 +38,68 @@ class TCache:
     __del__ = close
 
 
-class VerifyTile:
-    """One verify tile on one Engine.  collect=True records every publish
-    as (sig, frag bytes, ctl, tsorig); otherwise publishes are only counted."""
+GPU_MAX = 8   # FD_VERIFY_TILE_GPU_MAX
+LAT_BINS = 65536  # FD_VERIFY_TILE_LAT_BINS (1-us bins)
 
-    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True):
+
+class LatHist:
+    """fd_verify_tile_lat_t: a native publish callback's tsorig -> tspub
+    histogram (fd_verify_tile_lat_publish), no Python per publish."""
+
+    def __init__(self):
+        self.buf = np.zeros(4 + LAT_BINS, np.uint64)
+
+    @property
+    def fn(self):
+        return ctypes.cast(lib().fd_verify_tile_lat_publish, ctypes.c_void_p)
+
+    @property
+    def ctx(self):
+        return self.buf.ctypes.data
+
+    def reset(self):
+        self.buf[:] = 0
+
+    def summary(self) -> dict:
+        cnt, sum_ns, max_ns, over = (int(x) for x in self.buf[:4])
+        bins = self.buf[4:]
+        if not cnt:
+            return {"count": 0}
+        c = np.cumsum(bins)
+
+        def pct(q):
+            return float(np.searchsorted(c, q * cnt) + 0.5) * 1e-3   # ms, bin centre
+
+        return {"count": cnt, "mean_ms": sum_ns / cnt * 1e-6, "p50_ms": pct(0.5), "p99_ms": pct(0.99),
+                "p999_ms": pct(0.999), "max_ms": max_ns * 1e-6, "over_65ms": over}
+
+
+class VerifyTile:
+    """One verify tile on one Engine, or -- given a list of Engines -- on all
+    of them in the multi-engine feeder mode (fd_verify_tile_new_multi).
+    collect=True records every publish as (sig, frag bytes, ctl, tsorig);
+    lat=LatHist() records tsorig -> tspub natively instead; otherwise
+    publishes are only counted."""
+
+    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True, lat=None):
         self.engine = engine
         self.published = []
-        self._cb = PUBLISH_FN(self._on_publish) if collect else None
+        self._cb = PUBLISH_FN(self._on_publish) if collect and lat is None else None
         cfg = Cfg(batch_sigs, tcache_depth, tcache_map_cnt)
-        self._h = lib().fd_verify_tile_new(engine._h, ctypes.byref(cfg),
-                                           ctypes.cast(self._cb, ctypes.c_void_p) if self._cb else None, None)
+        cb = ctypes.cast(self._cb, ctypes.c_void_p) if self._cb else None
+        ctx = None
+        if lat is not None:                       # native latency histogram (LatHist)
+            cb, ctx = lat.fn, lat.ctx
+            self._lat = lat
+        if isinstance(engine, (list, tuple)):
+            L = lib()
+            L.fd_verify_tile_new_multi.restype = ctypes.c_void_p
+            L.fd_verify_tile_new_multi.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p]
+            arr = (ctypes.c_void_p * len(engine))(*[e._h for e in engine])
+            self._h = L.fd_verify_tile_new_multi(arr, len(engine), ctypes.byref(cfg), cb, ctx)
+        else:
+            self._h = lib().fd_verify_tile_new(engine._h, ctypes.byref(cfg), cb, ctx)
         if not self._h:
             raise EngineError(f"fd_verify_tile_new failed: {last_error()}")
 
@@ -69,6 +120,15 @@ class VerifyTile:
         err = lib().fd_verify_tile_rx_burst(self._h, _p(base), _p(off), _p(sz), c, t, len(off))
         if err:
             raise EngineError(f"rx_burst: {err}: {last_error()}")
+
+    def rx_burst_now(self, base: np.ndarray, off: np.ndarray, sz: np.ndarray):
+        """rx_burst with tsorig stamped at each frag's receipt"""
+        L = lib()
+        L.fd_verify_tile_rx_burst_now.argtypes = [ctypes.c_void_p] * 5
+        L.fd_verify_tile_rx_burst_now.restype = ctypes.c_int
+        err = L.fd_verify_tile_rx_burst_now(self._h, _p(base), _p(off), _p(sz), ctypes.c_void_p(len(off)))
+        if err:
+            raise EngineError(f"rx_burst_now: {err}: {last_error()}")
 
     def service(self, flush=False):
         err = lib().fd_verify_tile_service(self._h, 1 if flush else 0)
@@ -115,7 +175,8 @@ class Args(ctypes.Structure):
                 ("lazy_ns", ctypes.c_long),
                 ("close_fd_start", ctypes.c_uint), ("allow_syscalls_sz", ctypes.c_ushort),
                 ("allow_syscalls", ctypes.POINTER(ctypes.c_long)),
-                ("gpu", ctypes.c_void_p), ("tile", ctypes.c_void_p), ("err", ctypes.c_int)]
+                ("gpu", ctypes.c_void_p), ("tile", ctypes.c_void_p), ("err", ctypes.c_int),
+                ("device_cnt", ctypes.c_int), ("gpus", ctypes.c_void_p * GPU_MAX)]
 
 
 class TaskFns(ctypes.Structure):
@@ -129,7 +190,7 @@ class Task:
     another thread) or the task fails."""
 
     def __init__(self, frags, device=0, max_sigs=4096, max_blob=8 << 20, depth=3, batch_sigs=0,
-                 credits=None, lazy_ns=0):
+                 credits=None, lazy_ns=0, device_cnt=0):
         L = lib()
         L.fd_verify_tile_task_get.restype = ctypes.POINTER(TaskFns)
         fns = L.fd_verify_tile_task_get().contents
@@ -154,6 +215,7 @@ class Task:
         a.publish = ctypes.cast(self._pub, ctypes.c_void_p)
         a.cr_avail = ctypes.cast(self._cr, ctypes.c_void_p) if self._cr else None
         a.lazy_ns = lazy_ns
+        a.device_cnt = device_cnt
         self.args = a
 
     def _on_in(self, ctx, frag, sz, ctl, tsorig):

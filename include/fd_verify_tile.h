@@ -87,6 +87,24 @@ fd_verify_tile_new( fd_ed25519_gpu_t *           gpu,
                     fd_verify_tile_publish_fn    publish,
                     void *                       ctx );
 
+/* Multi-engine (feeder) mode: one tile driving gpu_cnt engines (at most
+   FD_VERIFY_TILE_GPU_MAX, e.g. one per GPU of the node), each through its
+   per-GPU feeder thread (fd_ed25519_gpu_feeder_*, NUMA-pinned, whole ring
+   in flight).  Batches are built in host buffers owned per engine (2 x its
+   ring depth, registered with it so the feeder DMAs them in place) and go
+   to the engines round robin; publishes stay in arrival order.  Same
+   semantics and counters as fd_verify_tile_new; RING_FULL_CNT counts waits
+   for a free batch buffer.  The engines must outlive the tile.  Lets the
+   reference's verify_tile_count (src/app/fdctl/config/default.toml:297-299)
+   stay independent of the GPU count. */
+#define FD_VERIFY_TILE_GPU_MAX (8)
+fd_verify_tile_t *
+fd_verify_tile_new_multi( fd_ed25519_gpu_t * const *   gpus,
+                          unsigned long                gpu_cnt,
+                          fd_verify_tile_cfg_t const * cfg,
+                          fd_verify_tile_publish_fn    publish,
+                          void *                       ctx );
+
 void fd_verify_tile_delete( fd_verify_tile_t * tile );
 
 /* Receive one frag.  Returns 0 if consumed (staged, or dropped by HA
@@ -109,6 +127,29 @@ fd_verify_tile_rx_burst( fd_verify_tile_t *    tile,
                          uint64_t const *      ctl,
                          uint64_t const *      tsorig,
                          unsigned long         n );
+
+/* fd_verify_tile_rx_burst with each frag's tsorig taken at its receipt
+   (CLOCK_MONOTONIC ns, the clock of the publish's tspub): a stream whose
+   publishes carry the tile's own tsorig -> tspub latency, as the
+   reference's synthetic-load tile stamps tsorig and tspub per frag
+   (src/app/frank/load/fd_frank_verify_synth_load.c:404-406). */
+int
+fd_verify_tile_rx_burst_now( fd_verify_tile_t *    tile,
+                             uint8_t const *       frag_base,
+                             uint64_t const *      off,
+                             uint32_t const *      sz,
+                             unsigned long         n );
+
+/* Diagnostics: a publish callback (ctx = fd_verify_tile_lat_t *) that
+   records each published frag's tspub - tsorig in 1-us bins (the last
+   bin and `over` catch >= 65.535 ms). */
+#define FD_VERIFY_TILE_LAT_BINS (65536UL)
+typedef struct {
+  unsigned long cnt, sum_ns, max_ns, over;
+  unsigned long bin[ FD_VERIFY_TILE_LAT_BINS ];
+} fd_verify_tile_lat_t;
+void fd_verify_tile_lat_publish( void * ctx, unsigned long sig, void const * frag, unsigned long sz,
+                                 unsigned long ctl, unsigned long tsorig, unsigned long tspub );
 
 /* Housekeeping: publish every completed batch without blocking; if
    flush, also submit the partial batch and wait for all in flight. */
@@ -169,6 +210,12 @@ typedef struct {
   fd_ed25519_gpu_t *         gpu;
   fd_verify_tile_t *         tile;
   int                        err;                   /* 0, or why init / run failed */
+  /* multi-engine mode (set by the caller): device_cnt > 1 gives the tile
+     one engine on each of devices device, device+1, ... (mod the gfx950
+     device count) in feeder mode (fd_verify_tile_new_multi); init fills
+     gpus[0..device_cnt) (gpu = gpus[0]) */
+  int                        device_cnt;
+  fd_ed25519_gpu_t *         gpus[ FD_VERIFY_TILE_GPU_MAX ];
 } fd_verify_tile_args_t;
 
 typedef struct {

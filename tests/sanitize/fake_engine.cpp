@@ -57,6 +57,12 @@ extern "C" void fake_engine_fail_submit( fd_ed25519_gpu_t * g, int code ) { std:
 /* the HIP calls of the feeder (C linkage, as hip_runtime_api.h declares them) */
 extern "C" int hipDeviceGetPCIBusId( char * bus, int len, int device ) { (void)bus; (void)len; (void)device; return 1; }
 extern "C" int hipSetDevice( int device ) { (void)device; return 0; }
+/* host regions (the verify tile's feeder mode registers its batch
+   buffers): nothing to map on the CPU */
+extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsigned long sz ) { return ( !g || !host || !sz ) ? FD_ED25519_ERR_ARG : 0; }
+extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) { return ( !g || !host ) ? FD_ED25519_ERR_ARG : 0; }
+/* the node the multi-engine tests pretend to have */
+extern "C" int fd_ed25519_gpu_device_cnt( void ) { return 8; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g->max_sigs; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g->max_blob; }
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g->depth; }

@@ -4,4 +4,5 @@
 #include "fuzz_verify_tile.cpp"
 #include "../../firedancer_amd/csrc/fd_verify_tile.cpp"
 #include "fake_engine.cpp"
+#include "feeder_stub.cpp"
 #include "../../firedancer_amd/csrc/fd_ed25519_gpu_desc.cpp"

@@ -129,3 +129,25 @@ def test_tile_task_cnc_asan_and_tsan(built, ref, tmp_path):
         r = subprocess.run([os.path.join(built, exe), str(p)], capture_output=True, env=env, timeout=300)
         assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
         assert r.stdout.startswith(b"ok "), exe
+
+
+def test_tile_multi_engine_asan_and_tsan(built, ref, tmp_path):
+    """The verify tile's multi-engine feeder mode (fd_verify_tile_new_multi:
+    one tile, 8 engines behind 8 feeder threads -- the 8-GPU node) on 8
+    fake engines: publish stream and counters equal the single-engine
+    tile's at two batch sizes with every engine used; the tile task with
+    device_cnt 8 driven over its cnc; a wedged engine fails the tile's
+    drain with ERR_GPU after the timeout -- under ASan/UBSan and
+    ThreadSanitizer."""
+    from test_verify_tile import make_stream
+    frags = make_stream(1200, 95, ref)
+    p = tmp_path / "frags.bin"
+    with open(p, "wb") as f:
+        f.write(struct.pack("<I", len(frags)))
+        for fr in frags:
+            f.write(struct.pack("<I", len(fr)) + fr)
+    env = dict(ENV, TSAN_OPTIONS="halt_on_error=1")
+    for exe in ("san_tile_multi", "tsan_tile_multi"):
+        r = subprocess.run([os.path.join(built, exe), str(p)], capture_output=True, env=env, timeout=400)
+        assert r.returncode == 0, (exe, r.stderr[-3000:].decode(errors="replace"))
+        assert r.stdout.startswith(b"ok "), exe

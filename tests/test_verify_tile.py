@@ -155,3 +155,32 @@ def test_tile_burst_counts_only(engine):
     assert d["PUB_CNT"] == len(frags) and d["SIG_CNT"] == 20000 and d["SV_FILT_CNT"] == 0
     assert d["BATCH_CNT"] >= 3
     tile.close()
+
+
+@pytest.mark.gpu
+def test_tile_multi_engine_vs_reference(ref):
+    """The multi-engine feeder mode (fd_verify_tile_new_multi) with three
+    engines on this box's GPU: every batch goes through an engine's feeder,
+    publishes and counters equal the reference's per-frag semantics, in
+    arrival order"""
+    frags = make_stream(6000, 333, ref)
+    exp_pub, exp, nsig = expected_for(frags, ref)
+    engines = [fa.Engine(0, 1024, 4 << 20, depth=2) for _ in range(3)]
+    try:
+        tile = VerifyTile(engines, batch_sigs=512)
+        for i, f in enumerate(frags):
+            tile.rx(f, ctl=i, tsorig=1000 + i)
+            if i % 61 == 0:
+                tile.service()
+        tile.service(flush=True)
+        assert [(s, f) for s, f, _, _ in tile.published] == exp_pub
+        ctl = [c for _, _, c, _ in tile.published]
+        assert ctl == sorted(ctl)
+        d = tile.diag()
+        for k, v in exp.items():
+            assert d[k] == v, k
+        assert d["PUB_CNT"] == len(exp_pub) and d["SIG_CNT"] == nsig and d["BATCH_CNT"] >= 3
+        tile.close()
+    finally:
+        for e in engines:
+            e.close()

@@ -77,6 +77,29 @@ def test_task_stream_vs_reference(ref):
 
 
 @pytest.mark.gpu
+def test_task_multi_engine_vs_reference(ref):
+    """device_cnt = 2: the task makes one engine per device (both on this
+    box's one GPU) and runs the tile in feeder mode; same publishes and
+    counters as the reference's per-frag semantics"""
+    frags = make_stream(3000, 79, ref)
+    exp_pub, exp, nsig = expected_for(frags, ref)
+    task = T.Task(frags, batch_sigs=512, max_sigs=1024, max_blob=4 << 20, depth=2, device_cnt=2)
+    assert task.init() == 0
+    try:
+        assert task.args.gpus[0] and task.args.gpus[1] and task.args.gpu == task.args.gpus[0]
+        assert _run_task(task) == 0
+        assert task.cnc.signal == T.SIGNAL_BOOT
+        assert [(s, f) for s, f, _, _ in task.published] == exp_pub
+        d = task.diag()
+        for k, v in exp.items():
+            assert d[k] == v, k
+        assert d["PUB_CNT"] == len(exp_pub) and d["SIG_CNT"] == nsig
+    finally:
+        task.fini()
+    assert not task.args.gpu and not task.args.gpus[1]
+
+
+@pytest.mark.gpu
 def test_task_backpressure_diag(ref):
     """no downstream credits for the first housekeeping rounds: IN_BACKP set
     and BACKP_CNT counted (fd_frank_verify.c:185-194), then the stream

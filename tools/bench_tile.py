@@ -6,6 +6,11 @@ host-fed from its own thread pinned to its GPU's NUMA node, PCIe
 included.  Prints one JSON line: sustained verifies/s and txns/s over
 --seconds of streaming.
 
+--latency: each frag's tsorig is its receipt time and the publish
+callback (native) histograms tsorig -> tspub; --curve 4096,16384,...
+prints one such point per batch size.  --multi: ONE tile in the
+multi-engine feeder mode over all the engines (fd_verify_tile_new_multi).
+
 Multi-GPU, one process: --gpus N runs --tiles tiles on each of devices
 0..N-1 (tile k on device k mod N), every tile an independent replica on
 its own engine, ring and frag stream (no collective on the data path).
@@ -32,7 +37,22 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--tiles", type=int, default=1, help="verify tiles per GPU (one host thread + engine each)")
     ap.add_argument("--gpus", type=int, default=1, help="devices driven from this process, one tile set each")
+    ap.add_argument("--multi", action="store_true",
+                    help="one tile in the multi-engine feeder mode driving --tiles engines on each of --gpus devices")
+    ap.add_argument("--latency", action="store_true",
+                    help="stamp tsorig at each frag's receipt and report tsorig -> tspub percentiles (native histogram)")
+    ap.add_argument("--curve", default="", help="comma-separated batch sizes: one latency point per size (implies --latency)")
     a = ap.parse_args()
+    if a.curve:
+        a.latency = True
+        for bs in [int(x) for x in a.curve.split(",")]:
+            a.batch = bs
+            run(a)
+        return
+    run(a)
+
+
+def run(a):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -65,10 +85,20 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but {ndev} gfx950 devices visible")
     devs = [local if world > 1 else (k % a.gpus) % max(ndev, 1) for k in range(a.tiles * a.gpus)]
     engs = [fa.Engine(d, max_sigs=a.batch, max_blob=a.batch * 1400, depth=a.depth) for d in devs]
-    tiles = [VerifyTile(e, batch_sigs=a.batch, collect=False) for e in engs]
+    from firedancer_amd.tile import LatHist
+    if a.multi:       # one tile, every engine behind its feeder
+        lats = [LatHist()] if a.latency else [None]
+        tiles = [VerifyTile(engs, batch_sigs=a.batch, collect=False, lat=lats[0])]
+        devs = devs[:1]
+    else:
+        lats = [LatHist() if a.latency else None for _ in engs]
+        tiles = [VerifyTile(e, batch_sigs=a.batch, collect=False, lat=h) for e, h in zip(engs, lats)]
     for tile in tiles:
         tile.rx_burst(base, off, sz)            # warm-up pass
         tile.service(flush=True)
+    for h in lats:
+        if h is not None:
+            h.reset()
     d0s = [tile.diag() for tile in tiles]
     if dist:
         dist.barrier()
@@ -82,7 +112,10 @@ def main():
             os.sched_setaffinity(0, cpus[devs[k]])
         # ctypes drops the GIL inside rx_burst: the tiles' host feeds run in parallel
         while time.perf_counter() - t0 < a.seconds:
-            tiles[k].rx_burst(base, off, sz)
+            if a.latency:
+                tiles[k].rx_burst_now(base, off, sz)
+            else:
+                tiles[k].rx_burst(base, off, sz)
             passes[k] += 1
         tiles[k].service(flush=True)
     th = [threading.Thread(target=feed, args=(k,)) for k in range(len(tiles))]
@@ -119,12 +152,29 @@ def main():
                           "frags_per_pass": len(frags), "sigs_per_pass": a.sigs,
                           "sig_dist": "uniform 1..12 per txn, 1232-byte txns", "pcie_inclusive": True,
                           "sv_filt_per_pass": int(d0["SV_FILT_CNT"]),
+                          "multi_engine_tile": bool(a.multi), "engines": len(engs),
+                          "latency_tsorig_to_tspub": lat_summary(lats) if a.latency else None,
                           "diag": d1}), flush=True)
-    for tile, e in zip(tiles, engs):
+    for tile in tiles:
         tile.close()
+    for e in engs:
         e.close()
     if dist:
         dist.destroy_process_group()
+
+
+def lat_summary(lats):
+    """merge the tiles' histograms: tsorig (frag received) -> tspub
+    (published after its batch's codes reached the host), PCIe included"""
+    from firedancer_amd.tile import LatHist
+    m = LatHist()
+    for h in lats:
+        m.buf[0] += h.buf[0]
+        m.buf[1] += h.buf[1]
+        m.buf[2] = max(m.buf[2], h.buf[2])
+        m.buf[3] += h.buf[3]
+        m.buf[4:] += h.buf[4:]
+    return m.summary()
 
 
 if __name__ == "__main__":
