@@ -113,7 +113,7 @@ static __device__ __forceinline__ void
 fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
               fd_ed25519_gpu_desc_t const * __restrict__ desc,
               int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-              uint8_t * sha_stage, uint64_t * __restrict__ kout, int sigmajor ) {
+              fd_lds_u8 * sha_stage, uint64_t * __restrict__ kout, int sigmajor ) {
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
   /* a descriptor outside the blob is reported, never dereferenced (the
@@ -173,12 +173,80 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
   } else op_start[i] = fd_recode( sw, kw, ops + i, n );
 }
 
+/* fd_prep_body on a wave pair (the latency path's front end, fd_k_front):
+   wave 0 runs the S check, the SHA-512 rounds (fd_sha2_rounds), sc_reduce
+   and the recoder; wave 1 feeds it the message words and schedule
+   (fd_sha2_schedule).  Same results as fd_prep_body (signature-major op
+   rows); no early return before the barrier loops end. */
+FD_DEV int fd_wave_max( int x ) {
+#pragma unroll
+  for( int o=32; o>0; o>>=1 ) { int y = __shfl_xor( x, o, 64 ); x = y > x ? y : x; }
+  return x;
+}
+static __device__ __forceinline__ void
+fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+               fd_ed25519_gpu_desc_t const * __restrict__ desc,
+               int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
+               fd_lds_u8 * stage, fd_sha2_lds_ring * ring ) {
+  uint32_t const wv = threadIdx.x >> 6;
+  bool live = i < n;
+  fd_ed25519_gpu_desc_t d = live ? desc[i] : fd_ed25519_gpu_desc_t{ 0, 0, 0, 0 };
+  bool in = live && fd_desc_in( d, blob_sz );
+  uint8_t const * R = blob + (in ? d.sig_off : 0u);
+  uint8_t const * S = R + 32;
+  uint8_t const * A = blob + (in ? d.pub_off : 0u);
+  uint8_t const * M = blob + (in ? d.msg_off : 0u);
+  uint32_t sz = in ? d.msg_sz : 0u;
+  uint32_t sw[8];
+  int st = FD_ED25519_ERR_ARG;
+  if( in ) {
+    fd_ld32( sw, S );
+    uint32_t s31 = sw[7] >> 24;
+    /* S range check (fd_ed25519_user.c:372-393), as fd_prep_body */
+    st = FD_ST_PENDING;
+    if( s31 > 0x10u ) st = FD_ED25519_ERR_SIG;
+    else if( s31 == 0x10u ) {
+      if( sw[4] | sw[5] | sw[6] | (sw[7] & 0x00ffffffu) ) st = strict ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
+      else {
+        uint64_t lo = ((uint64_t)sw[1] << 32) | sw[0], hi = ((uint64_t)sw[3] << 32) | sw[2];
+        uint64_t llo = 0x5812631a5cf5d3edULL, lhi = 0x14def9dea2f79cd6ULL;
+        if( hi > lhi || (hi == lhi && lo >= llo) ) st = FD_ED25519_ERR_SIG;
+      }
+    }
+  }
+  bool pend = st == FD_ST_PENDING;
+  uint32_t nblk = pend ? (uint32_t)((64ULL + sz + 17ULL + 127ULL) >> 7) : 0u;
+  uint32_t nmax = (uint32_t)__builtin_amdgcn_readfirstlane( fd_wave_max( (int)nblk ) );
+  if( wv ) {     /* the message / schedule wave */
+    fd_sha2_schedule( ring, stage, pend, R, A, M, sz, nblk, nmax );
+    return;
+  }
+  uint64_t dig[8];
+#pragma unroll
+  for( int j=0; j<8; j++ ) dig[j] = fd_gpu_sha512_iv[0][j];
+  fd_sha2_rounds( dig, ring, nblk, nmax );
+  if( !live ) return;
+  status[i] = st;
+  if( !pend ) { op_start[i] = FD_OPS_MAX; return; }
+#pragma unroll
+  for( int j=0; j<8; j++ ) dig[j] = fd_bswap64( dig[j] );
+  uint64_t k[4];
+  fd_sc_reduce( k, dig );
+  uint32_t kw[8];
+#pragma unroll
+  for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
+  int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
+#pragma unroll
+  for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
+  op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
+}
+
 extern "C" __global__ void __launch_bounds__(256, 4)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
            uint64_t * __restrict__ kout ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
-  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, kout, 0 );
+  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, kout, 0 );
 }
 
 /* ------------------------------------------------------------------ */
@@ -338,23 +406,31 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
    no data dependence once decomp stops skipping failed S checks, so one
    launch runs both side by side -- blocks [0, nb_prep) prep, the rest
    decomp -- and a small batch's front end takes max(prep, decomp)
-   instead of their sum.  One wave per block (FD_FRONT_WAVES 1): with
-   several batches in flight the dispatcher can then put a front-end wave
-   on an idle SIMD; a 4-wave block always puts one of its waves on the
-   SIMD of a resident quad-DSM wave of another batch, and the block (so
-   the front end) ran at that shared SIMD's pace (111 -> 225-280 us,
-   depth-3 trace, tools/lat_trace3.py). */
+   instead of their sum.  Small blocks: with several batches in flight
+   the dispatcher can then put a front-end wave on an idle SIMD; a 4-wave
+   block always puts one of its waves on the SIMD of a resident quad-DSM
+   wave of another batch, and the block (so the front end) ran at that
+   shared SIMD's pace (111 -> 225-280 us, depth-3 trace,
+   tools/lat_trace3.py).  Round 3: two-wave blocks, prep as a wave pair
+   (fd_prep2_body; decomp blocks then hold 128 points). */
+/* FD_PREP2 1: prep blocks are wave pairs (fd_prep2_body: one wave runs
+   the SHA-512 rounds, its partner the message words and schedule), decomp
+   blocks two waves of points; 0: one-wave blocks, one lane per signature
+   (fd_prep_body) */
+#ifndef FD_PREP2
+#define FD_PREP2 1
+#endif
 #ifndef FD_FRONT_WAVES
-#define FD_FRONT_WAVES 1
+#define FD_FRONT_WAVES (FD_PREP2 ? 2 : 1)
 #endif
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only (tools/front_stamps.py): histograms of the
    front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
    bins) for prep and decomp waves, accumulated over every launch with
    vector atomics */
-__device__ unsigned long long fd_front_hist[2][256];
+__device__ unsigned long long fd_front_hist[3][256];   /* prep (round wave), decomp, prep schedule wave */
 extern "C" hipError_t fd_ed25519_gpu_front_hist( void * host, int clear ) {
-  if( clear ) { static unsigned long long z[2][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  if( clear ) { static unsigned long long z[3][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
   return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_front_hist), sizeof(fd_front_hist), 0, hipMemcpyDeviceToHost );
 }
 #endif
@@ -362,22 +438,32 @@ extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
 fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
+#if FD_PREP2
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_SHA_STAGE_BYTES];   /* the schedule wave's */
+  __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
+#else
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
+#endif
 #ifdef FD_FRONT_PRIO
   __builtin_amdgcn_s_setprio( FD_FRONT_PRIO );   /* experiment: issue ahead of co-resident quad-DSM waves */
 #endif
 #ifdef FD_FRONT_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if( blockIdx.x < nb_prep )
-    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, NULL, 1 );
-  else
+  if( blockIdx.x < nb_prep ) {
+#if FD_PREP2
+    fd_prep2_body( (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u), n, blob, blob_sz, desc, status, ops, op_start, strict,
+                   (fd_lds_u8 *)sha_stage, (fd_sha2_lds_ring *)&sha_ring );
+#else
+    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, NULL, 1 );
+#endif
+  } else
     fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
 #ifdef FD_FRONT_STAMPS
   __builtin_amdgcn_wave_barrier();
   unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;      /* 10 ns ticks */
   unsigned b = (unsigned)(dt / 200ULL); if( b > 255u ) b = 255u;
-  if( (threadIdx.x & 63u) == 0u ) atomicAdd( &fd_front_hist[blockIdx.x < nb_prep ? 0 : 1][b], 1ULL );
+  if( (threadIdx.x & 63u) == 0u ) atomicAdd( &fd_front_hist[blockIdx.x < nb_prep ? ((threadIdx.x >> 6) ? 2 : 0) : 1][b], 1ULL );
 #endif
 }
 
@@ -1624,7 +1710,7 @@ fd_k_sha512_batch( uint64_t n, uint8_t const * __restrict__ blob, fd_ed25519_gpu
   uint64_t st[8];
 #pragma unroll
   for( int k=0; k<8; k++ ) st[k] = fd_gpu_sha512_iv[is384 ? 1 : 0][k];
-  fd_sha512_blocks<0>( st, NULL, NULL, blob + d.msg_off, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
+  fd_sha512_blocks<0>( st, NULL, NULL, blob + d.msg_off, d.msg_sz, (fd_lds_u8 *)sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
   int nw = is384 ? 6 : 8;
 #pragma unroll
   for( int k=0; k<8; k++ ) if( k < nw ) out[8*i + k] = fd_bswap64( st[k] );
@@ -1674,7 +1760,8 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   if( quad ) {
     /* latency path: prep and decomp in one launch (their time lands in phase 1) */
     unsigned const bt = 64u*FD_FRONT_WAVES;
-    unsigned const fp = (unsigned)((n + bt - 1) / bt), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
+    unsigned const ps = FD_PREP2 ? 64u : bt;   /* signatures per prep block */
+    unsigned const fp = (unsigned)((n + ps - 1) / ps), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
     hipLaunchKernelGGL( fd_k_front, dim3(fp + fd), dim3(bt), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start,
                         w->pstat, w->pts, portable, strict, fp );
     if( ev ) hipEventRecord( ev[1], stream );

@@ -192,14 +192,20 @@ __constant__ static uint64_t const fd_gpu_sha512_iv[2][8] = {
    stage + 1024 (q>>2) + 16 l + 4 (q&3).  Chunks at or past the message end
    are not fetched (the batch blob is readable 16 bytes past its end, so
    the last fetched chunk never leaves it). */
+/* LDS pointers are typed as such (address space 3): passed as generic
+   pointers, the LDS-DMA builtin's destination needs an address-space cast
+   that ROCm 7.2's LLVM lowers with an aperture compare it then rejects
+   ("Operand has incorrect register class", V_CMP_NE_U32 0, src_shared_base)
+   in some inlining shapes (the two-wave front end, stamps builds) */
+typedef __attribute__((address_space(3))) uint8_t fd_lds_u8;
 #define FD_SHA_CHUNKS      9
 #define FD_SHA_STAGE_BYTES (FD_SHA_CHUNKS*1024)
 
-FD_DEV void fd_sha_stage( uint8_t * stage, uint8_t const * win, uint8_t const * end ) {
+FD_DEV void fd_sha_stage( fd_lds_u8 * stage, uint8_t const * win, uint8_t const * end ) {
 #pragma unroll
   for( int c=0; c<FD_SHA_CHUNKS; c++ )
     if( win + 16*c < end )
-      __builtin_amdgcn_global_load_lds( (void const *)(win + 16*c), (void *)(stage + 1024*c), 16, 0, 0 );
+      __builtin_amdgcn_global_load_lds( (void const *)(win + 16*c), (__attribute__((address_space(3))) void *)(stage + 1024*c), 16, 0, 0 );
 }
 
 /* Message words FIRST..15 of a block from its staged dwords (word i is
@@ -238,7 +244,7 @@ FD_DEV void fd_sha_words( uint64_t (&w)[16], uint32_t const (&dw)[33], uint32_t 
 /* Read back the 33 staged dwords of a block whose first message byte is
    at window byte d: dword dq+4m+r of the window is at
    stage + off[r] + 1024 m (immediate offsets). */
-FD_DEV void fd_sha_read( uint32_t (&dw)[33], uint8_t const * stage, uint32_t d ) {
+FD_DEV void fd_sha_read( uint32_t (&dw)[33], fd_lds_u8 const * stage, uint32_t d ) {
   uint32_t lane = threadIdx.x & 63u, dq = d >> 2, off[4];
 #pragma unroll
   for( int r=0; r<4; r++ ) {
@@ -247,13 +253,13 @@ FD_DEV void fd_sha_read( uint32_t (&dw)[33], uint8_t const * stage, uint32_t d )
   }
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
 #pragma unroll
-  for( int k=0; k<33; k++ ) dw[k] = *(uint32_t const *)( stage + off[k & 3] + 1024u*(uint32_t)(k >> 2) );
+  for( int k=0; k<33; k++ ) dw[k] = *(__attribute__((address_space(3))) uint32_t const *)( stage + off[k & 3] + 1024u*(uint32_t)(k >> 2) );
 }
 
 /* The block's words are formed (its staged dwords dead) before the next
    block's DMA may overwrite the stage; then compression runs while the
    DMA is in flight. */
-FD_DEV void fd_sha_next( uint64_t (&w)[16], uint8_t * stage, uint8_t const * win, uint8_t const * end, bool more ) {
+FD_DEV void fd_sha_next( uint64_t (&w)[16], fd_lds_u8 * stage, uint8_t const * win, uint8_t const * end, bool more ) {
 #pragma unroll
   for( int i=0; i<16; i++ ) asm volatile( "" : "+v"(w[i]) );
   asm volatile( "s_waitcnt lgkmcnt(0)" ::: "memory" );
@@ -264,7 +270,7 @@ FD_DEV uint8_t const * fd_floor16( uint8_t const * p ) { return (uint8_t const *
 
 template<int PRE>
 FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz,
-                              uint8_t * stage ) {
+                              fd_lds_u8 * stage ) {
   uint64_t L = (uint64_t)PRE + sz;                   /* bytes hashed */
   uint32_t nblk = (uint32_t)((L + 17ULL + 127ULL) >> 7);
   uint8_t const * end = M + sz;
@@ -294,11 +300,127 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
   }
 }
 
+/* ---- SHA-512 on a wave pair (the latency path's front end) -------------
+
+   One wave of a two-wave workgroup runs the 80 rounds of every block; its
+   partner forms the message words (LDS-DMA staged, as above) and the
+   message schedule W[16..79] and hands them over through an LDS ring of
+   two 8-word chunks, synchronised by workgroup barriers:
+     producer:  write chunk k into slot k%2, barrier k
+     consumer:  barrier k, read chunk k from slot k%2, 8 rounds
+   so the producer writes chunk k+1 while the consumer runs chunk k, and
+   slot (k+1)%2 was last read (chunk k-1) before barrier k.  Both waves
+   run the same 10 barriers per block over the same wave-uniform block
+   count (the longest message of the wave's 64 signatures); a lane past
+   its own last block computes on don't-care words and its state is not
+   updated.  The round wave's block drops from ~3,570 to ~2,400
+   instructions (the schedule's rotates and 64-bit adds move to the
+   partner).  Measured on lone 4096-signature batches: round waves 98 ->
+   89 us, the front end 0.103 -> 0.095 ms (profiles/r03_front_two_wave.jsonl;
+   a three-slot ring that prefetches the next chunk measured 92 us). */
+#define FD_SHA2_CW     8                     /* words per chunk */
+#define FD_SHA2_CHUNKS (80/FD_SHA2_CW)       /* chunks per block */
+struct fd_sha2_ring { uint64_t w[2][FD_SHA2_CW][64]; };   /* 8 KiB, lane-contiguous (no bank conflicts) */
+typedef __attribute__((address_space(3))) fd_sha2_ring fd_sha2_lds_ring;
+
+#define FD_SHA_ROUND_W(wj,kt) do {                                                 \
+    uint64_t hkw = fd_opaque64u( h + (kt) + (wj) );                             \
+    uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
+    uint64_t ch = fd_ch64( e, f, g );                                             \
+    uint64_t t1 = fd_opaque64u( hkw + ch ) + S1;                                \
+    uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
+    uint64_t mj = fd_maj64( a, b, c );                                          \
+    uint64_t t2 = fd_opaque64u( S0 + mj );                                      \
+    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+t2;                              \
+  } while(0)
+
+/* the round wave: st (IV on entry) advanced over the lane's own nblk blocks */
+FD_DEV void fd_sha2_rounds( uint64_t (&st)[8], fd_sha2_lds_ring * ring, uint32_t nblk, uint32_t nblk_max ) {
+  uint32_t const lane = threadIdx.x & 63u;
+  uint32_t k = 0;
+  for( uint32_t blk=0; blk<nblk_max; blk++ ) {
+    uint64_t a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
+    /* rolled: each chunk's 8 round constants are one scalar load (an
+       unrolled block keeps all 80 live in SGPRs and spills them) */
+#pragma unroll 1
+    for( int ch=0; ch<FD_SHA2_CHUNKS; ch++ ) {
+      __syncthreads();
+      uint64_t W[FD_SHA2_CW];
+#pragma unroll
+      for( int j=0; j<FD_SHA2_CW; j++ ) W[j] = ring->w[k & 1u][j][lane];
+#pragma unroll
+      for( int j=0; j<FD_SHA2_CW; j++ ) FD_SHA_ROUND_W( W[j], fd_gpu_sha512_k[FD_SHA2_CW*ch + j] );
+      k++;
+    }
+    bool upd = blk < nblk;
+    st[0] = upd ? st[0]+a : st[0]; st[1] = upd ? st[1]+b : st[1]; st[2] = upd ? st[2]+c : st[2]; st[3] = upd ? st[3]+d : st[3];
+    st[4] = upd ? st[4]+e : st[4]; st[5] = upd ? st[5]+f : st[5]; st[6] = upd ? st[6]+g : st[6]; st[7] = upd ? st[7]+h : st[7];
+  }
+}
+
+/* the partner wave: message words of R || A || M(sz) (PRE = 64) and the
+   schedule, chunk by chunk into the ring; live lanes only stage and read
+   message bytes (stage: this wave's FD_SHA_STAGE_BYTES of LDS) */
+FD_DEV void fd_sha2_schedule( fd_sha2_lds_ring * ring, fd_lds_u8 * stage, bool live, uint8_t const * R, uint8_t const * A,
+                              uint8_t const * M, uint32_t sz, uint32_t nblk, uint32_t nblk_max ) {
+  uint32_t const lane = threadIdx.x & 63u;
+  uint64_t L = 64ULL + sz;
+  uint8_t const * end = M + sz;
+  uint64_t w[16];
+  uint32_t dw[33];
+#pragma unroll
+  for( int i=0; i<16; i++ ) w[i] = 0ULL;
+  uint32_t k = 0;
+  if( live ) fd_sha_stage( stage, fd_floor16( M ), end );
+  for( uint32_t blk=0; blk<nblk_max; blk++ ) {
+    bool on = live && blk < nblk;
+    if( blk == 0u ) {
+      if( live ) {
+#pragma unroll
+        for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
+#pragma unroll
+        for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
+      }
+      uint32_t d = (uint32_t)((uintptr_t)M & 15u);
+      fd_sha_read( dw, stage, d );
+      fd_sha_words<8, 64>( w, dw, (d & 3u) * 8u, -64, sz, L, nblk == 1u );
+      fd_sha_next( w, stage, fd_floor16( M + 64 ), end, live && nblk > 1u );
+    } else {
+      /* the block index as a VGPR value: with the wave-uniform (SGPR) loop
+         counter LLVM (ROCm 7.2) selects a scalar operand where a vector one
+         is required in the staging address math and fails with "Operand has
+         incorrect register class" */
+      uint32_t const bv = (uint32_t)fd_opaque( (int32_t)blk );
+      int64_t mbase = (int64_t)bv*128 - 64;
+      uint32_t d = (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 15u);
+      fd_sha_read( dw, stage, d );
+      fd_sha_words<0, 64>( w, dw, (d & 3u) * 8u, mbase, sz, L, bv == nblk-1u );
+      fd_sha_next( w, stage, fd_floor16( M + mbase + 128 ), end, on && bv + 1u < nblk );
+    }
+#pragma unroll
+    for( int ch=0; ch<FD_SHA2_CHUNKS; ch++ ) {
+#pragma unroll
+      for( int j=0; j<FD_SHA2_CW; j++ ) {
+        int const t = FD_SHA2_CW*ch + j;
+        if( t >= 16 ) {
+          uint64_t w15 = w[(t+1)&15], w2 = w[(t+14)&15];
+          uint64_t s0 = fd_xor3_64( fd_rotr64(w15,1), fd_rotr64(w15,8), fd_shr64(w15,7) );
+          uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
+          w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
+        }
+        ring->w[k & 1u][j][lane] = w[t&15];
+      }
+      __syncthreads();
+      k++;
+    }
+  }
+}
+
 /* SHA-512 of R(32) || A(32) || M(sz) (fd_ed25519_user.c:411-414).
    Returns the digest as 8 words where word i holds digest bytes
    8i..8i+7 little endian. */
 FD_DEV void fd_sha512_ram( uint64_t (&dig)[8], uint8_t const * R, uint8_t const * A, uint8_t const * M, uint32_t sz,
-                          uint8_t * stage ) {
+                          fd_lds_u8 * stage ) {
   uint64_t st[8];
 #pragma unroll
   for( int i=0; i<8; i++ ) st[i] = fd_gpu_sha512_iv[0][i];
