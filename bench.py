@@ -489,6 +489,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         lat = (st["t_done_ns"] - st["t_push_ns"]) * 1e-6
         qlat = (st["t_done_ns"] - st["t_submit_ns"]) * 1e-6
         hop = (st["t_submit_ns"] - st["t_push_ns"]) * 1e-6
+        pick = (st["t_pick_ns"] - st["t_push_ns"]) * 1e-6      # the feeder's pickup
+        enq = (st["t_submit_ns"] - st["t_pick_ns"]) * 1e-6     # staging + HIP enqueue of the batch
         c = st["codes"].sum(axis=0)
         hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
         res = {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
@@ -501,6 +503,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                "submit_to_done_p99_ms": float(np.percentile(qlat, 99)),
                "push_to_submit_p50_ms": float(np.percentile(hop, 50)),
                "push_to_submit_p99_ms": float(np.percentile(hop, 99)),
+               "push_to_pick_p50_ms": float(np.percentile(pick, 50)), "push_to_pick_p99_ms": float(np.percentile(pick, 99)),
+               "pick_to_submit_p50_ms": float(np.percentile(enq, 50)), "pick_to_submit_p99_ms": float(np.percentile(enq, 99)),
                "codes": hist, "codes_ok": valid_corpus_ok(hist, nb * BATCH_SIGS) and bool((st["state"] == 1).all())}
         if period_ns:
             sl = (st["t_done_ns"] - st["t_sched_ns"]) * 1e-6

@@ -477,12 +477,13 @@ class Job(ctypes.Structure):
     """fd_ed25519_gpu_job_t"""
     _fields_ = [("n", ctypes.c_ulong), ("blob", ctypes.c_void_p), ("blob_sz", ctypes.c_ulong),
                 ("desc", ctypes.c_void_p), ("out", ctypes.c_void_p), ("state", ctypes.c_int),
-                ("t_push_ns", ctypes.c_ulong), ("t_submit_ns", ctypes.c_ulong), ("t_done_ns", ctypes.c_ulong)]
+                ("t_push_ns", ctypes.c_ulong), ("t_submit_ns", ctypes.c_ulong), ("t_done_ns", ctypes.c_ulong),
+                ("t_pick_ns", ctypes.c_ulong)]
 
 
 # fd_ed25519_gpu_synth_stat_t
 SYNTH_STAT_DTYPE = np.dtype([("t_sched_ns", "<u8"), ("t_push_ns", "<u8"), ("t_submit_ns", "<u8"), ("t_done_ns", "<u8"),
-                             ("state", "<i4"), ("codes", "<u4", (5,))], align=True)
+                             ("t_pick_ns", "<u8"), ("state", "<i4"), ("codes", "<u4", (5,))], align=True)
 
 
 class Feeder:

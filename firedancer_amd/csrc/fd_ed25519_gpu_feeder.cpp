@@ -167,6 +167,7 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
         std::lock_guard<std::mutex> g( f->lock );
         if( f->queue.empty() ) break;
         pending = f->queue.front(); f->queue.pop_front();
+        pending->t_pick_ns = fd_feeder_now();
       }
       int r = fd_feeder_submit( f, pending );
       if( r == 0 ) break;
@@ -249,7 +250,7 @@ FD_EXPORT int fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * f
 
 FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
   if( !f || !j || j->n > f->max_sigs || (j->n && (!j->desc || !j->out)) || (j->blob_sz && !j->blob) ) return FD_ED25519_ERR_ARG;
-  j->t_push_ns = fd_feeder_now(); j->t_submit_ns = 0; j->t_done_ns = 0;
+  j->t_push_ns = fd_feeder_now(); j->t_submit_ns = 0; j->t_done_ns = 0; j->t_pick_ns = 0;
   if( !j->n ) { fd_job_finish( j, 1 ); return 0; }
   __atomic_store_n( &j->state, 0, __ATOMIC_RELEASE );
   {

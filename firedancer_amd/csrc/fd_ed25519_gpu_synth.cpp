@@ -51,6 +51,7 @@ static void fd_synth_record( fd_ed25519_gpu_synth_stat_t * st, fd_ed25519_gpu_jo
   st->t_push_ns   = j->t_push_ns;
   st->t_submit_ns = j->t_submit_ns;
   st->t_done_ns   = j->t_done_ns;
+  st->t_pick_ns   = j->t_pick_ns;
   st->state       = j->state;
   for( int c=0; c<5; c++ ) st->codes[c] = 0;
   if( j->state != 1 ) return;

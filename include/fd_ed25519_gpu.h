@@ -386,7 +386,9 @@ int fd_ed25519_gpu_device_cnt( void );
    A job is owned by the caller; blob, desc and out must stay valid until
    its state is nonzero: 1 = codes in out[0..n), < 0 = FD_ED25519_ERR_*
    (nothing written).  t_*_ns are CLOCK_MONOTONIC stamps of push, submit
-   (H2D enqueued) and completion (codes on the host). */
+   (the whole batch enqueued: H2D, kernels, D2H), completion (codes on the
+   host) and pick (the feeder took the job off its queue, before staging
+   and enqueueing it). */
 
 typedef struct fd_ed25519_gpu_job {
   unsigned long                 n;
@@ -396,6 +398,7 @@ typedef struct fd_ed25519_gpu_job {
   int *                         out;
   int                           state;     /* written by the feeder (atomic release) */
   unsigned long                 t_push_ns, t_submit_ns, t_done_ns;
+  unsigned long                 t_pick_ns;
 } fd_ed25519_gpu_job_t;
 
 typedef struct fd_ed25519_gpu_feeder fd_ed25519_gpu_feeder_t;
@@ -429,7 +432,7 @@ int  fd_ed25519_gpu_job_wait        ( fd_ed25519_gpu_job_t const * job, long tim
    or the first job error (FD_ED25519_ERR_GPU if a job did not complete
    within 30 s). */
 typedef struct fd_ed25519_gpu_synth_stat {
-  unsigned long t_sched_ns, t_push_ns, t_submit_ns, t_done_ns;
+  unsigned long t_sched_ns, t_push_ns, t_submit_ns, t_done_ns, t_pick_ns;
   int           state;
   unsigned int  codes[5];
 } fd_ed25519_gpu_synth_stat_t;
