@@ -1600,7 +1600,14 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
          step) */
       if( kind ) {
         fe4 vt; fd_pool_ld( vt, L, s );
+#ifdef FD_POOL_TRAFFIC_DIAG
+        /* diagnostic builds only (tools/pmc_pool_split.sh): every Ai read
+           hits signature 0's entries (cache resident), so the HBM bytes
+           that disappear are the Ai-entry reads; codes are wrong */
+        fd_pool_add( vt, op, tab, FD_TAB_ENTRY, fd_gpu_bi_tab );
+#else
         fd_pool_add( vt, op, tab + sg*FD_TAB_ENTRY, n*FD_TAB_ENTRY, fd_gpu_bi_tab );
+#endif
         fd_pool_st( L, s, vt );
       } else {
         fe4 vt; fd_pool_ld( vt, L, s );
