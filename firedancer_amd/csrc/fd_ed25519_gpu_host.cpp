@@ -961,11 +961,25 @@ static unsigned long       fd_default_blob = 1UL << 26;
 static fd_ed25519_gpu_t * fd_default_engine( void );
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_default( void ) { return fd_default_engine(); }
 
+/* The default engine is released at exit, ahead of the HIP runtime's own
+   teardown (its destructors were registered when it loaded, so they run
+   after this handler): left to the runtime's teardown, its streams and
+   pinned buffers crashed process exit under rocprofv3
+   (profiles/r03_per_signature_timeline.json). */
+static void fd_default_engine_fini( void ) {
+  std::lock_guard<std::mutex> guard( fd_default_lock );
+  fd_ed25519_gpu_t * g = fd_default_gpu;
+  fd_default_gpu = NULL;
+  if( g ) fd_ed25519_gpu_delete( g );
+}
+
 static fd_ed25519_gpu_t * fd_default_engine( void ) {
   std::lock_guard<std::mutex> guard( fd_default_lock );
   if( !fd_default_gpu ) {
     char const * dev = getenv( "FD_ED25519_GPU_DEVICE" );
     fd_default_gpu = fd_ed25519_gpu_new( dev ? atoi( dev ) : 0, fd_default_sigs, fd_default_blob );
+    static int fini_set = 0;
+    if( fd_default_gpu && !fini_set ) { fini_set = 1; atexit( fd_default_engine_fini ); }
   }
   return fd_default_gpu;
 }

@@ -367,7 +367,8 @@ int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
 char const * fd_ed25519_gpu_last_error( void );
 
 /* The process-default engine behind fd_ed25519_verify (created on first
-   use on $FD_ED25519_GPU_DEVICE, default 0); NULL without a device. */
+   use on $FD_ED25519_GPU_DEVICE, default 0); NULL without a device.  It
+   belongs to the library (released at exit): never delete it. */
 fd_ed25519_gpu_t * fd_ed25519_gpu_default( void );
 
 /* Number of usable gfx950 devices visible to this process. */
