@@ -218,7 +218,12 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   uint32_t nblk = pend ? (uint32_t)((64ULL + sz + 17ULL + 127ULL) >> 7) : 0u;
   uint32_t nmax = (uint32_t)__builtin_amdgcn_readfirstlane( fd_wave_max( (int)nblk ) );
   if( wv ) {     /* the message / schedule wave */
+#if FD_PREP2_DIRECT
+    (void)stage;
+    fd_sha2_schedule_direct( ring, pend, R, A, M, sz, nblk, nmax );
+#else
     fd_sha2_schedule( ring, stage, pend, R, A, M, sz, nblk, nmax );
+#endif
     return;
   }
   uint64_t dig[8];
@@ -423,6 +428,12 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
 #ifndef FD_FRONT_WAVES
 #define FD_FRONT_WAVES (FD_PREP2 ? 2 : 1)
 #endif
+/* FD_PREP2_DIRECT 1: the schedule wave fetches message bytes into
+   registers (fd_sha2_schedule_direct), so a front-end block holds only
+   the 8 KiB chunk ring */
+#ifndef FD_PREP2_DIRECT
+#define FD_PREP2_DIRECT 1
+#endif
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only (tools/front_stamps.py): histograms of the
    front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
@@ -438,7 +449,10 @@ extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
 fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
-#if FD_PREP2
+#if FD_PREP2 && FD_PREP2_DIRECT
+  __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
+  fd_lds_u8 * const sha_stage = NULL;
+#elif FD_PREP2
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_SHA_STAGE_BYTES];   /* the schedule wave's */
   __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
 #else

@@ -416,6 +416,77 @@ FD_DEV void fd_sha2_schedule( fd_sha2_lds_ring * ring, fd_lds_u8 * stage, bool l
   }
 }
 
+/* The partner wave without LDS staging: each block's 144-byte window is
+   fetched straight into registers (9 x 16-byte loads from the dword
+   floor of the block's first byte, so the realignment shift is
+   (address & 3) * 8 and no per-lane register index is needed), one block
+   ahead.  The front end's blocks then hold only the 8 KiB chunk ring:
+   two fit on a CU beside four quad-DSM waves of the previous batch of its
+   CU group (with the 9 KiB stage, one did, and a 4,096-signature front
+   end ran in two rounds there, profiles/r03_ring_trace.json).  Chunks at
+   or past the message end are not fetched (zeros), as when staged. */
+FD_DEV void fd_sha_fetch( uint32_t (&dw)[36], uint8_t const * base4, uint8_t const * end, bool on ) {
+#pragma unroll
+  for( int c=0; c<9; c++ ) {
+    uint32_t a = 0u, b = 0u, x = 0u, y = 0u;
+    if( on && base4 + 16*c < end ) {
+      uint32_t const * q = (uint32_t const *)(base4 + 16*c);
+      a = q[0]; b = q[1]; x = q[2]; y = q[3];
+    }
+    dw[4*c] = a; dw[4*c+1] = b; dw[4*c+2] = x; dw[4*c+3] = y;
+  }
+}
+FD_DEV uint8_t const * fd_floor4( uint8_t const * p ) { return (uint8_t const *)((uintptr_t)p & ~(uintptr_t)3); }
+
+FD_DEV void fd_sha2_schedule_direct( fd_sha2_lds_ring * ring, bool live, uint8_t const * R, uint8_t const * A,
+                                     uint8_t const * M, uint32_t sz, uint32_t nblk, uint32_t nblk_max ) {
+  uint32_t const lane = threadIdx.x & 63u;
+  uint64_t L = 64ULL + sz;
+  uint8_t const * end = M + sz;
+  uint64_t w[16];
+  uint32_t dw[36];
+#pragma unroll
+  for( int i=0; i<16; i++ ) w[i] = 0ULL;
+  uint32_t k = 0;
+  fd_sha_fetch( dw, fd_floor4( M ), end, live );
+  for( uint32_t blk=0; blk<nblk_max; blk++ ) {
+    bool on = live && blk < nblk;
+    uint32_t const bv = (uint32_t)fd_opaque( (int32_t)blk );
+    if( blk == 0u ) {
+      if( live ) {
+#pragma unroll
+        for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
+#pragma unroll
+        for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
+      }
+      uint32_t const (&d33)[33] = *(uint32_t const (*)[33])dw;
+      fd_sha_words<8, 64>( w, d33, (uint32_t)((uintptr_t)M & 3u) * 8u, -64, sz, L, nblk == 1u );
+      fd_sha_fetch( dw, fd_floor4( M + 64 ), end, live && nblk > 1u );
+    } else {
+      int64_t mbase = (int64_t)bv*128 - 64;
+      uint32_t const (&d33)[33] = *(uint32_t const (*)[33])dw;
+      fd_sha_words<0, 64>( w, d33, (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 3u) * 8u, mbase, sz, L, bv == nblk-1u );
+      fd_sha_fetch( dw, fd_floor4( M + mbase + 128 ), end, on && bv + 1u < nblk );
+    }
+#pragma unroll
+    for( int ch=0; ch<FD_SHA2_CHUNKS; ch++ ) {
+#pragma unroll
+      for( int j=0; j<FD_SHA2_CW; j++ ) {
+        int const t = FD_SHA2_CW*ch + j;
+        if( t >= 16 ) {
+          uint64_t w15 = w[(t+1)&15], w2 = w[(t+14)&15];
+          uint64_t s0 = fd_xor3_64( fd_rotr64(w15,1), fd_rotr64(w15,8), fd_shr64(w15,7) );
+          uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
+          w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
+        }
+        ring->w[k & 1u][j][lane] = w[t&15];
+      }
+      __syncthreads();
+      k++;
+    }
+  }
+}
+
 /* SHA-512 of R(32) || A(32) || M(sz) (fd_ed25519_user.c:411-414).
    Returns the digest as 8 words where word i holds digest bytes
    8i..8i+7 little endian. */
