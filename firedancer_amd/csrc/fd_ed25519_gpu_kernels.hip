@@ -183,6 +183,12 @@ FD_DEV int fd_wave_max( int x ) {
   for( int o=32; o>0; o>>=1 ) { int y = __shfl_xor( x, o, 64 ); x = y > x ? y : x; }
   return x;
 }
+/* FD_PREP2_DIRECT 1: the schedule wave fetches message bytes into
+   registers (fd_sha2_schedule_direct), so a front-end block holds only
+   the 8 KiB chunk ring */
+#ifndef FD_PREP2_DIRECT
+#define FD_PREP2_DIRECT 1
+#endif
 static __device__ __forceinline__ void
 fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
                fd_ed25519_gpu_desc_t const * __restrict__ desc,
@@ -427,12 +433,6 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
 #endif
 #ifndef FD_FRONT_WAVES
 #define FD_FRONT_WAVES (FD_PREP2 ? 2 : 1)
-#endif
-/* FD_PREP2_DIRECT 1: the schedule wave fetches message bytes into
-   registers (fd_sha2_schedule_direct), so a front-end block holds only
-   the 8 KiB chunk ring */
-#ifndef FD_PREP2_DIRECT
-#define FD_PREP2_DIRECT 1
 #endif
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only (tools/front_stamps.py): histograms of the
