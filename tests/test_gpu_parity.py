@@ -321,6 +321,31 @@ def test_quad_equals_uniform(engine, uniform, n):
     assert (q == u).all(), np.nonzero(q != u)[0][:10]
 
 
+def test_quad_messages_at_every_alignment(engine, uniform):
+    """the latency front end (fd_k_front) reads each message at its own byte
+    alignment: the same signatures packed with every start offset mod 16 of
+    sig, pub and message, through the quad schedule and the uniform one
+    (fd_k_prep's front end), all valid.  (A build whose schedule wave lost
+    its staging buffer still passed the golden corpora, whose messages sit
+    16-aligned, and rejected every unaligned one.)"""
+    base = corpus.solana_txns(512, seed=91)
+    trip = [(base.msg(i), base.sig(i), base.pub(i)) for i in range(len(base))]
+    parts, desc, off = [], np.zeros(len(trip), corpus.DESC_DTYPE), 0
+    for i, (m, sg, pb) in enumerate(trip):
+        pad = (i * 7) % 16 + (i // 16) % 3          # every residue mod 16, with the fields at mixed offsets
+        parts.append(b"\x55" * pad)
+        off += pad
+        desc[i] = (off, off + 64, off + 96 + (i % 5), len(m))
+        parts.append(bytes(sg) + bytes(pb) + b"\xaa" * (i % 5) + bytes(m))
+        off += 96 + (i % 5) + len(m)
+    blob = np.frombuffer(b"".join(parts) + b"\0" * 64, np.uint8).copy()
+    assert len(set((desc["msg_off"] % 16).tolist())) == 16
+    assert engine.dsm_quad_max >= len(desc)
+    q = engine.verify_packed(blob, desc)
+    u = uniform.verify_packed(blob, desc)
+    assert (q == 0).all() and (u == 0).all(), (np.nonzero(q)[0][:8], np.nonzero(u)[0][:8])
+
+
 def test_quad_q2_vectors(engine):
     """the reference-quirk (Q2) and RFC 8032 vectors through the quad
     schedule explicitly"""
