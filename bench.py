@@ -20,7 +20,10 @@ Extra measurements on rank 0 at N=1:
   latency      C2 at its own granularity: 4096-signature batches streamed
                through the per-GPU feeder and the engine's pinned ring
                (PCIe both ways included): verifies/s and push -> codes-on-
-               host p50/p99 at ring depth 6 (4 CU groups), 4 and 1
+               host p50/p99 on a ring of depth 8 over 4 CU groups with 6
+               (the main point), 5, 7 and 8 batches in flight, depth 4,
+               depth 1, offered 40 M/s open loop, and the best closed-loop
+               point whose p99 stayed within 1 ms
   cpu_baseline the reference's own fd_ed25519_verify (oracle/_ref build,
                'reference') or the CPU restatement ('port') on a bounded
                sample of the same corpus, all host threads of this rank
