@@ -211,9 +211,10 @@ FD_DEV void fd_sha_stage( fd_lds_u8 * stage, uint8_t const * win, uint8_t const 
 /* Message words FIRST..15 of a block from its staged dwords (word i is
    window bytes d + 8 (i - FIRST) .. +7), with the padding byte and the
    bit count of the final block. */
-template<int FIRST, int PRE>
-FD_DEV void fd_sha_words( uint64_t (&w)[16], uint32_t const (&dw)[33], uint32_t sh, int64_t mbase, uint32_t sz,
+template<int FIRST, int PRE, int N>
+FD_DEV void fd_sha_words( uint64_t (&w)[16], uint32_t const (&dw)[N], uint32_t sh, int64_t mbase, uint32_t sz,
                           uint64_t L, bool last ) {
+  static_assert( N >= 33, "a block's words read 33 dwords" );
 #pragma unroll
   for( int i=FIRST; i<16; i++ ) {
     int j = i - FIRST;
@@ -459,13 +460,11 @@ FD_DEV void fd_sha2_schedule_direct( fd_sha2_lds_ring * ring, bool live, uint8_t
 #pragma unroll
         for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
       }
-      uint32_t const (&d33)[33] = *(uint32_t const (*)[33])dw;
-      fd_sha_words<8, 64>( w, d33, (uint32_t)((uintptr_t)M & 3u) * 8u, -64, sz, L, nblk == 1u );
+      fd_sha_words<8, 64>( w, dw, (uint32_t)((uintptr_t)M & 3u) * 8u, -64, sz, L, nblk == 1u );
       fd_sha_fetch( dw, fd_floor4( M + 64 ), end, live && nblk > 1u );
     } else {
       int64_t mbase = (int64_t)bv*128 - 64;
-      uint32_t const (&d33)[33] = *(uint32_t const (*)[33])dw;
-      fd_sha_words<0, 64>( w, d33, (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 3u) * 8u, mbase, sz, L, bv == nblk-1u );
+      fd_sha_words<0, 64>( w, dw, (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 3u) * 8u, mbase, sz, L, bv == nblk-1u );
       fd_sha_fetch( dw, fd_floor4( M + mbase + 128 ), end, on && bv + 1u < nblk );
     }
 #pragma unroll
