@@ -304,7 +304,9 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
 /* ---- SHA-512 on a wave pair (the latency path's front end) -------------
 
    One wave of a two-wave workgroup runs the 80 rounds of every block; its
-   partner forms the message words (LDS-DMA staged, as above) and the
+   partner forms the message words (fetched into registers a block ahead,
+   fd_sha2_schedule_direct below; fd_sha2_schedule stages them through LDS
+   as above, the FD_PREP2_DIRECT 0 build) and the
    message schedule W[16..79] and hands them over through an LDS ring of
    two 8-word chunks, synchronised by workgroup barriers:
      producer:  write chunk k into slot k%2, barrier k
