@@ -189,6 +189,12 @@ FD_DEV int fd_wave_max( int x ) {
 #ifndef FD_PREP2_DIRECT
 #define FD_PREP2_DIRECT 1
 #endif
+#ifdef FD_FRONT_STAMPS
+/* diagnostic builds only: [0] prep round wave, [1] decomp, [2] prep
+   schedule wave, [3] prep round wave up to its digest (the rest of [0] is
+   sc_reduce, the recoder and the op row) -- per-wave times in 2 us bins */
+__device__ unsigned long long fd_front_hist[4][256];
+#endif
 static __device__ __forceinline__ void
 fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
                fd_ed25519_gpu_desc_t const * __restrict__ desc,
@@ -235,7 +241,18 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   uint64_t dig[8];
 #pragma unroll
   for( int j=0; j<8; j++ ) dig[j] = fd_gpu_sha512_iv[0][j];
+#ifdef FD_FRONT_STAMPS
+  unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
   fd_sha2_rounds( dig, ring, nblk, nmax );
+#ifdef FD_FRONT_STAMPS
+  {
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long dt = __builtin_amdgcn_s_memrealtime() - ts0;
+    unsigned b = (unsigned)(dt / 200ULL); if( b > 255u ) b = 255u;
+    if( (threadIdx.x & 63u) == 0u ) atomicAdd( &fd_front_hist[3][b], 1ULL );
+  }
+#endif
   if( !live ) return;
   status[i] = st;
   if( !pend ) { op_start[i] = FD_OPS_MAX; return; }
@@ -439,9 +456,8 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
    front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
    bins) for prep and decomp waves, accumulated over every launch with
    vector atomics */
-__device__ unsigned long long fd_front_hist[3][256];   /* prep (round wave), decomp, prep schedule wave */
 extern "C" hipError_t fd_ed25519_gpu_front_hist( void * host, int clear ) {
-  if( clear ) { static unsigned long long z[3][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  if( clear ) { static unsigned long long z[4][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
   return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_front_hist), sizeof(fd_front_hist), 0, hipMemcpyDeviceToHost );
 }
 #endif

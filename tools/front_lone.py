@@ -39,11 +39,11 @@ def main():
     L.fd_ed25519_gpu_front_hist(None, 1)
     ks = np.array([eng.verify_dev_timed(n, d_blob.data_ptr(), len(blob), d_desc.data_ptr(), d_out.data_ptr(), s)
                    for _ in range(reps)])
-    h = np.zeros((3, 256), np.uint64)
+    h = np.zeros((4, 256), np.uint64)   # fd_front_hist[4][256]
     L.fd_ed25519_gpu_front_hist(h.ctypes.data, 0)
     out = {"lib": os.environ.get("FD_ED25519_LIB", "default"), "front_ms": float(np.median(ks[:, 0])),
            "accepted": int((d_out == 0).sum().item())}
-    for k, name in enumerate(("prep_rounds", "decomp", "prep_schedule")):
+    for k, name in enumerate(("prep_rounds", "decomp", "prep_schedule", "prep_rounds_to_digest")):
         c = h[k].astype(np.float64)
         us = (np.arange(256) + 0.5) * 2.0
         tot = c.sum()

@@ -26,13 +26,13 @@ def main():
     L = fa.lib()
     L.fd_ed25519_gpu_front_hist.argtypes = [ctypes.c_void_p, ctypes.c_int]
     base = corpus.solana_txns(bench.UNIQUE_SIGS, seed=1000, nthreads=16)
-    h = np.zeros((2, 256), np.uint64)
+    h = np.zeros((4, 256), np.uint64)   # fd_front_hist[4][256]
     L.fd_ed25519_gpu_front_hist(None, 1)
     r = bench.ring_stream(fa, base, 0, nb, depth, groups=min(depth, 4), window=window)
     L.fd_ed25519_gpu_front_hist(h.ctypes.data, 0)
     out = {"depth": depth, "window": window, "p50_ms": r["p50_ms"], "p99_ms": r["p99_ms"],
            "group_always": os.environ.get("FD_ED25519_GPU_GROUP_ALWAYS", "0")}
-    for k, name in enumerate(("prep", "decomp")):
+    for k, name in enumerate(("prep", "decomp", "prep_schedule_wave", "prep_round_wave_to_digest")):
         c = h[k].astype(np.float64)
         us = (np.arange(256) + 0.5) * 2.0
         tot = c.sum()
