@@ -17,13 +17,16 @@ RCCL only carries the timing barrier and the max-over-ranks.
 Extra measurements on rank 0 at N=1:
   roofline     per-kernel HIP-event durations over the timed launches,
                algorithmic int32 ops / duration
-  latency      C2 at its own granularity: 4096-signature batches streamed
-               through the per-GPU feeder and the engine's pinned ring
-               (PCIe both ways included): verifies/s and push -> codes-on-
-               host p50/p99 on a ring of depth 8 over 4 CU groups with 6
-               (the main point), 5, 7 and 8 batches in flight, depth 4,
-               depth 1, offered 40 M/s open loop, and the best closed-loop
-               point whose p99 stayed within 1 ms
+  latency      C2 at its own granularity: 4096-signature batches of a
+               C3-mix ring corpus (10 % invalid + the Q2 vectors in every
+               batch) streamed through the per-GPU feeder and the engine's
+               pinned ring (PCIe both ways included): closed loop (6 -- the
+               main point --, 5, 7, 8 outstanding on a depth-8 ring, depth
+               4, depth 1; push -> codes-on-host p50/p99), and an open-loop
+               sweep of offered loads (25-40 M verifies/s) whose latency is
+               scheduled arrival -> codes on the host; the headline is the
+               highest offered load sustained at sched -> done p99 <= 1 ms.
+               Every code of every leg is compared with the reference's.
   cpu_baseline the reference's own fd_ed25519_verify (oracle/_ref build,
                'reference') or the CPU restatement ('port') on a bounded
                sample of the same corpus, all host threads of this rank
@@ -430,34 +433,11 @@ def main():
                             "VALU-bound, traffic is a secondary check",
         }
         if not a.no_latency:
-            # C2 at its own granularity: 4096-signature batches through the
-            # per-GPU feeder and pinned ring, PCIe both ways included
-            res["latency"] = ring_stream(fa, base, local, a.latency_batches, a.ring_depth, window=a.ring_window)
-            # one more batch in flight: more throughput, p99 just above 1 ms
-            res["latency"]["throughput_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
-                                                             window=min(a.ring_window + 1, a.ring_depth))
-            res["latency"]["window5_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
-                                                          window=max(a.ring_window - 1, 1))
-            res["latency"]["window8_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
-                                                          window=a.ring_depth)
-            res["latency"]["lower_latency_point"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), 4)
-            # one batch in flight at a time: the per-batch floor
-            res["latency"]["depth1"] = ring_stream(fa, base, local, max(a.latency_batches // 5, 20), 1)
-            # open loop: batches offered at a fixed 40 M verifies/s (one per
-            # 102.4 us), at most the ring's depth outstanding
-            res["latency"]["paced_40M"] = ring_stream(fa, base, local, max(a.latency_batches // 2, 20), a.ring_depth,
-                                                      window=a.ring_depth, period_ns=int(BATCH_SIGS / 40e6 * 1e9))
-            res["ring_4096_verifies_per_s"] = res["latency"]["pcie_inclusive_verifies_per_s"]
-            # the closed-loop points read as one curve: the most throughput
-            # whose push -> done p99 stayed within 1 ms on this box
+            res["latency"] = latency_legs(fa, corpus, a, local)
             lat = res["latency"]
-            pts = [lat] + [lat[k] for k in ("throughput_point", "window5_point", "window8_point", "lower_latency_point", "depth1")]
-            ok = [p for p in pts if p["p99_ms"] <= 1.0 and p["codes_ok"]]
-            best = max(ok, key=lambda p: p["pcie_inclusive_verifies_per_s"]) if ok else None
-            lat["best_under_p99_1ms"] = None if best is None else {
-                "verifies_per_s": best["pcie_inclusive_verifies_per_s"], "p99_ms": best["p99_ms"], "p50_ms": best["p50_ms"],
-                "window": best["window"], "ring_depth": best["ring_depth"]}
-            res["ring_4096_best_verifies_per_s_at_p99_le_1ms"] = None if best is None else best["pcie_inclusive_verifies_per_s"]
+            res["ring_4096_verifies_per_s"] = lat["pcie_inclusive_verifies_per_s"]
+            res["ring_4096_best_verifies_per_s_at_p99_le_1ms"] = (lat["best_under_p99_1ms"] or {}).get("verifies_per_s")
+            res["ring_4096_max_offered_at_sched_p99_le_1ms"] = lat["max_offered_at_sched_p99_le_1ms"]
         if not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, usable_cores())
             # the checker: the reference build's codes for the whole step corpus
@@ -471,8 +451,82 @@ def main():
         dist.destroy_process_group()
 
 
-def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, quad2=None, period_ns=0,
-                lat_dsm=None):
+# the C2 ring's corpus: RING_WINDOWS windows of one batch each, the C3 mix
+# (10 % invalid over every case of corpus.CASES) plus the three SURVEY Q2
+# vectors at fixed offsets of every window (only a limb-exact engine rejects
+# them), so every timed ring batch carries reference evidence
+RING_WINDOWS = 64
+RING_Q2_AT = (1024, 2048, 4095)
+# offered loads of the open-loop sweep, M verifies/s
+PACED_MPS = (25, 30, 32, 34, 36, 38, 40)
+
+
+def ring_reference_codes(ring, threads):
+    """The reference build's codes for the ring corpus (the checker; computed
+    before the ring legs, compared with each leg's codes after it is timed)."""
+    import ctypes
+    ref = os.path.join(ROOT, "oracle", "_ref", "libfdref.so")
+    if not os.path.exists(ref):
+        return None
+    sig, pub, data, off, sz = ring.flat()
+    exp = np.zeros(len(ring), np.int32)
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    ctypes.CDLL(ref).ref_verify_batch(ctypes.c_uint64(len(ring)), P(sig), P(pub), P(data), P(off), P(sz), P(exp), threads)
+    return exp
+
+
+def latency_legs(fa, corpus, a, device):
+    """C2 at its own granularity, PCIe both ways: closed-loop points (batches
+    outstanding 5-8 on a depth-8 ring, depth 4, depth 1) and an open-loop
+    sweep of offered loads (PACED_MPS) whose latency is scheduled arrival ->
+    codes on the host.  Every code of every leg is compared with the
+    reference build's after the leg."""
+    t0 = time.time()
+    ring = corpus.c3_windows(RING_WINDOWS, BATCH_SIGS, seed=4242, extra=[
+        (bytes.fromhex(m), bytes.fromhex(s), bytes.fromhex(p)) for m, s, p in corpus.Q2_VECTORS],
+        extra_at=RING_Q2_AT, nthreads=min(16, os.cpu_count() or 8))
+    gen_s = time.time() - t0
+    t0 = time.time()
+    exp = ring_reference_codes(ring, usable_cores())
+    ref_s = time.time() - t0
+    nb, nb2 = a.latency_batches, max(a.latency_batches // 2, 20)
+    lat = ring_stream(fa, ring, device, nb, a.ring_depth, window=a.ring_window, expected=exp)
+    lat["corpus"] = {"windows": RING_WINDOWS, "sigs": len(ring), "q2_at": list(RING_Q2_AT), "gen_s": gen_s,
+                     "reference_codes": None if exp is None else codes_hist(exp), "reference_s": ref_s,
+                     "content": "C3 mix at C2 shape: 1232-byte txns, 10 % of the signatures corrupted over all 18 "
+                                "invalid cases, the 3 SURVEY Q2 vectors at fixed offsets of every 4096-signature window"}
+    # closed loop: more / fewer batches outstanding, a shallower ring, one at a time
+    lat["throughput_point"] = ring_stream(fa, ring, device, nb2, a.ring_depth, window=min(a.ring_window + 1, a.ring_depth),
+                                          expected=exp)
+    lat["window5_point"] = ring_stream(fa, ring, device, nb2, a.ring_depth, window=max(a.ring_window - 1, 1), expected=exp)
+    lat["window8_point"] = ring_stream(fa, ring, device, nb2, a.ring_depth, window=a.ring_depth, expected=exp)
+    lat["lower_latency_point"] = ring_stream(fa, ring, device, nb2, 4, expected=exp)
+    lat["depth1"] = ring_stream(fa, ring, device, max(nb // 5, 20), 1, expected=exp)
+    pts = [lat] + [lat[k] for k in ("throughput_point", "window5_point", "window8_point", "lower_latency_point", "depth1")]
+    ok = [p for p in pts if p["p99_ms"] <= 1.0 and p["codes_ok"]]
+    best = max(ok, key=lambda p: p["pcie_inclusive_verifies_per_s"]) if ok else None
+    lat["best_under_p99_1ms"] = None if best is None else {
+        "verifies_per_s": best["pcie_inclusive_verifies_per_s"], "p99_ms": best["p99_ms"], "p50_ms": best["p50_ms"],
+        "window": best["window"], "ring_depth": best["ring_depth"], "latency": "push -> codes on the host (closed loop)"}
+    # open loop: one batch every period_ns, latency from its scheduled arrival
+    # (a batch the full ring holds back waits, and that wait is counted)
+    paced = []
+    for mps in PACED_MPS:
+        r = ring_stream(fa, ring, device, nb2, a.ring_depth, window=a.ring_depth,
+                        period_ns=int(round(BATCH_SIGS / (mps * 1e6) * 1e9)), expected=exp)
+        paced.append(r)
+    lat["paced"] = paced
+    held = [r for r in paced if r["sustained"] and r["sched_to_done_p99_ms"] <= 1.0 and r["codes_ok"]]
+    top = max(held, key=lambda r: r["offered_verifies_per_s"]) if held else None
+    lat["max_offered_at_sched_p99_le_1ms"] = None if top is None else top["offered_verifies_per_s"]
+    lat["max_offered_point"] = None if top is None else {
+        k: top[k] for k in ("offered_verifies_per_s", "pcie_inclusive_verifies_per_s", "sched_to_done_p50_ms",
+                            "sched_to_done_p99_ms", "p99_ms", "mismatches")}
+    return lat
+
+
+def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, period_ns=0,
+                expected=None):
     """C2 at its own granularity: nb 4096-signature batches streamed through
     one engine's pinned ring by its per-GPU feeder thread
     (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
@@ -481,26 +535,38 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
     lies with no staging memcpy.  The producer is the library's native
     synthetic-load loop (fd_ed25519_gpu_feeder_synth, the counterpart of
     the reference's synth-load verify tile): `window` batches outstanding
-    (closed loop), or one batch pushed every period_ns (paced, at most
-    `window` outstanding).  latency = push -> codes on the host."""
+    (closed loop; latency = push -> codes on the host), or one batch pushed
+    every period_ns (paced, at most `window` outstanding; latency =
+    scheduled arrival -> codes on the host).  Batch i is window
+    starts[i % 64] of `base` (one batch per BATCH_SIGS-signature window);
+    every code is returned and, with `expected` (the reference build's codes
+    for `base`), compared code by code after the timed run."""
     eng = fa.Engine(device, max_sigs=BATCH_SIGS, max_blob=8 << 20, depth=depth)
     try:
         if groups:
             eng.cu_groups = groups
-        if quad2 is not None:
-            eng.quad2 = quad2
-        if lat_dsm is not None:
-            eng.lat_dsm = lat_dsm
         if register:
             eng.register(base.blob)
         feeder = fa.Feeder(eng)
-        starts = np.random.default_rng(seed).integers(0, len(base) - BATCH_SIGS, 64)
+        nwin = len(base) // BATCH_SIGS
+        starts = np.random.default_rng(seed).permutation(nwin).astype(np.uint64) * BATCH_SIGS
         W = window or depth
         t0 = time.perf_counter()
-        st = feeder.synth(base.blob, base.desc, BATCH_SIGS, starts, nb, W, period_ns)
+        st, codes = feeder.synth(base.blob, base.desc, BATCH_SIGS, starts, nb, W, period_ns, codes=True)
         wall = time.perf_counter() - t0
         numa = feeder.numa_node
         feeder.close()
+        # the codes of EVERY batch (fill included) against the reference
+        c = st["codes"].sum(axis=0)
+        hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
+        complete = bool((st["state"] == 1).all()) and int(c.sum()) == nb * BATCH_SIGS and int(c[4]) == 0
+        mism = None
+        if expected is not None:
+            mism = 0
+            for s in range(min(len(starts), nb)):
+                rows = codes[s::len(starts)]
+                o = int(starts[s])
+                mism += int((rows != expected[o:o + BATCH_SIGS][None, :]).sum())
         skip = W if nb > 2 * W else 0          # the ring's fill
         st = st[skip:]
         lat = (st["t_done_ns"] - st["t_push_ns"]) * 1e-6
@@ -508,10 +574,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         hop = (st["t_submit_ns"] - st["t_push_ns"]) * 1e-6
         pick = (st["t_pick_ns"] - st["t_push_ns"]) * 1e-6      # the feeder's pickup
         enq = (st["t_submit_ns"] - st["t_pick_ns"]) * 1e-6     # staging + HIP enqueue of the batch
-        c = st["codes"].sum(axis=0)
-        hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
         res = {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
-               "cu_groups": eng.cu_groups, "quad2_policy": eng.quad2, "lat_dsm": eng.lat_dsm, "registered_source": bool(register),
+               "cu_groups": eng.cu_groups, "registered_source": bool(register),
                "feeder_numa_node": numa, "producer": "native (fd_ed25519_gpu_feeder_synth)",
                "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
@@ -522,12 +586,17 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                "push_to_submit_p99_ms": float(np.percentile(hop, 99)),
                "push_to_pick_p50_ms": float(np.percentile(pick, 50)), "push_to_pick_p99_ms": float(np.percentile(pick, 99)),
                "pick_to_submit_p50_ms": float(np.percentile(enq, 50)), "pick_to_submit_p99_ms": float(np.percentile(enq, 99)),
-               "codes": hist, "codes_ok": valid_corpus_ok(hist, nb * BATCH_SIGS) and bool((st["state"] == 1).all())}
+               "codes": hist, "reference_checked": expected is not None, "mismatches": mism,
+               "codes_ok": complete and (mism == 0 if expected is not None else True)}
         if period_ns:
             sl = (st["t_done_ns"] - st["t_sched_ns"]) * 1e-6
-            res.update(offered_verifies_per_s=BATCH_SIGS / (period_ns * 1e-9),
+            offered = BATCH_SIGS / (period_ns * 1e-9)
+            res.update(offered_verifies_per_s=offered,
+                       sustained=res["pcie_inclusive_verifies_per_s"] >= 0.98 * offered,
                        sched_to_done_p50_ms=float(np.percentile(sl, 50)),
-                       sched_to_done_p99_ms=float(np.percentile(sl, 99)))
+                       sched_to_done_p99_ms=float(np.percentile(sl, 99)),
+                       sched_to_done_max_ms=float(sl.max()),
+                       latency="scheduled arrival -> codes on the host (p50_ms/p99_ms: push -> codes)")
         return res
     finally:
         eng.close()

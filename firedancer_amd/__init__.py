@@ -98,7 +98,7 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_submit.restype = ip
         L.fd_ed25519_gpu_try_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fd_ed25519_gpu_try_submit.restype = ip
-        L.fd_ed25519_gpu_feeder_synth.argtypes = [vp, vp, ul, vp, ul, ul, vp, ul, ul, ip, ul, vp]
+        L.fd_ed25519_gpu_feeder_synth.argtypes = [vp, vp, ul, vp, ul, ul, vp, ul, ul, ip, ul, vp, vp]
         L.fd_ed25519_gpu_feeder_synth.restype = ip
         L.fd_ed25519_gpu_poll.argtypes = [vp, ul, vp, ip]
         L.fd_ed25519_gpu_poll.restype = ip
@@ -142,6 +142,12 @@ def lib() -> ctypes.CDLL:
         L.fd_verify_tile_rx.restype = ip
         L.fd_verify_tile_rx_burst.argtypes = [vp, vp, vp, vp, vp, vp, ul]
         L.fd_verify_tile_rx_burst.restype = ip
+        L.fd_verify_tile_rx_burst_now.argtypes = [vp, vp, vp, vp, ul]
+        L.fd_verify_tile_rx_burst_now.restype = ip
+        L.fd_verify_tile_new_multi.argtypes = [vp, ul, vp, vp, vp]
+        L.fd_verify_tile_new_multi.restype = vp
+        L.fd_verify_tile_new_inplace.argtypes = [vp, vp, vp, ul, vp, vp]
+        L.fd_verify_tile_new_inplace.restype = vp
         L.fd_verify_tile_service.argtypes = [vp, ip]
         L.fd_verify_tile_service.restype = ip
         L.fd_verify_tile_diag.argtypes = [vp, vp]
@@ -526,20 +532,23 @@ class Feeder:
             raise EngineError(f"job: {strerror(err)}: {last_error()}")
 
     def synth(self, blob: np.ndarray, desc: np.ndarray, batch_sigs: int, starts, nbatch: int, window: int,
-              period_ns: int = 0) -> np.ndarray:
+              period_ns: int = 0, codes: bool = False):
         """The native synthetic-load producer (fd_ed25519_gpu_feeder_synth): nbatch
         jobs of batch_sigs signatures, job i from desc[starts[i % len(starts)]:],
         closed loop with `window` outstanding (period_ns 0) or paced one job per
-        period_ns.  Returns the per-job SYNTH_STAT_DTYPE records."""
+        period_ns.  Returns the per-job SYNTH_STAT_DTYPE records, and with
+        codes=True also every code as int8 [nbatch, batch_sigs]."""
         blob = np.ascontiguousarray(blob, np.uint8)
         desc = np.ascontiguousarray(desc, DESC_DTYPE)
         st = np.ascontiguousarray(starts, np.uint64)
         stat = np.zeros(nbatch, SYNTH_STAT_DTYPE)
+        cs = np.full((nbatch, batch_sigs), 99, np.int8) if codes else None
         err = lib().fd_ed25519_gpu_feeder_synth(self._h, _p(blob), blob.nbytes, _p(desc), len(desc), batch_sigs,
-                                                _p(st), len(st), nbatch, window, period_ns, _p(stat))
+                                                _p(st), len(st), nbatch, window, period_ns, _p(stat),
+                                                _p(cs) if codes else None)
         if err:
             raise EngineError(f"feeder synth: {strerror(err)}: {last_error()}")
-        return stat
+        return (stat, cs) if codes else stat
 
     def close(self):
         if self._h:

@@ -288,6 +288,20 @@ def single_msg(n, msg_sz=256, seed=0, nthreads=8):
 
 
 # ---------------------------------------------------------------- adversarial
+# The three SURVEY.md section 8c (Q2) vectors as (msg, sig, pub) hex: valid
+# signatures that the reference's AVX2 build rejects (ERR_MSG) through its
+# limb compare of non-canonical coordinates (fd_ed25519_user.c:419-427).
+Q2_VECTORS = [
+    ("562c7b301299d47deefe44c5368b77333c214b79b3e7dc03b091f0add168c0910740ac7544423faa742c3ba3d5286c624e1c5174ae4ccad097bea9f3c3cc197f33b0c640b71ae479e30fb2b7159bfb099c9780aa80fff0c1ea9682838b906f8677ea561bef530df8f714bea2b6eeb81b7b468ab64220d9d62a00a557e66bb35d",
+     "a53f00568d07e4944ee86da222b258beae6d8353024faf57de1fa83b05eea496267f66788337eab61e0d36da454c46700ad217fb3cb08d3d016548e4ff5be803",
+     "5bba42a60de96030d8f6a85dc5809e3f39a210671f50ee0ffdab810e18725a49"),
+    ("b594272285085ae80737ae28cf824783a8788d96d301ef3376d5f6de6599498fe92ab86784c593a3d42802cb97dcd15797351268f765787d68e4b6053cef065acc426921518d814afde0ca82fd788941a87e9468af2070c05755a2caeb6bdd34b8d108fe1ae96d59f8017eb0fe18c1a6da300403730cc3344d8cf5ecdba1bce9",
+     "588e6a12357767161aae6b35a7768481883861dcb399c0929ba2319214871d93895b3ab2404066f4e92dba7c688dbca7874ef5c16bedcb1efc6eb50560fe3602",
+     "a8c5f0b9a0cad87801e0e550c7b4cda39c96cc31b6de89123437e41c3f42ccfe"),
+    ("fc2f6a47b996987a34e02bc58cc0e2f84144f1fa4a07d2964f2695e7daecdf8c1bb177623f9fe1d12b12a087383fa17153234d17507d1d45b5e009f968528efd7e51c1781977306ae975fee54e1665da6896fc2d53ce9ea9340282bbae55102db2dbaffb5798b0874037889b445e8b00afeeb1ad12f53e389f5cd7bc238bd4c9",
+     "f064a139d45ec0994e332d79364ddd8c2894a3a9b97b571e864efe0cf2fbae0055b9ce729e97564fe0bf3444b29719f1908388a5ff1807355cff0a69561fb003",
+     "1935951cae485585719b256b1132ccbc729da20b718cfe2950c18dcdd82bbd71")]
+
 CASES = [
     "valid", "flip_R", "flip_S", "flip_msg", "flip_pub", "S_eq_L", "S_eq_L1", "S_top_big",
     "S_q1_early_accept", "noncanon_A", "noncanon_R", "small_A", "small_R", "small_both",
@@ -407,3 +421,41 @@ def from_triples(triples):
         off += 96 + len(m)
     blob = np.frombuffer(b"".join(parts) + b"\0" * 64, np.uint8).copy()
     return Batch(blob, desc, np.zeros(len(triples), np.int8))
+
+
+def c3_windows(nwin, batch_sigs, seed, extra=None, extra_at=None, invalid_frac=0.1, nthreads=8):
+    """The C2 ring's corpus with the C3 mix (BASELINE configs[1] batches,
+    configs[2] content): nwin windows of batch_sigs signatures, each window
+    contiguous in the blob (so a ring batch moves one ~4 MB span), drawn
+    from adversarial_txns (invalid_frac corrupted over every case of CASES),
+    plus the (msg, sig, pub) triples `extra` (e.g. the SURVEY Q2 vectors,
+    which only the limb-exact path rejects) placed at the same offsets
+    `extra_at` of every window.  Window w is desc[w*batch_sigs:(w+1)*batch_sigs]."""
+    extra = list(extra or [])
+    extra_at = list(extra_at if extra_at is not None else [(j + 1) * batch_sigs // (len(extra) + 1) for j in range(len(extra))])
+    assert len(extra_at) == len(extra) and len(set(extra_at)) == len(extra_at) and all(0 <= a < batch_sigs for a in extra_at)
+    k = batch_sigs - len(extra)
+    adv = adversarial_txns(nwin * k, seed=seed, invalid_frac=invalid_frac, nthreads=nthreads)
+    q = from_triples(extra) if extra else None
+    parts = []
+    for w in range(nwin):
+        d = adv.desc[w * k:(w + 1) * k].copy()
+        lo = int(min(d["sig_off"].min(), d["pub_off"].min(), d["msg_off"].min()))
+        hi = int(max((d["sig_off"].astype(np.int64) + 64).max(), (d["pub_off"].astype(np.int64) + 32).max(),
+                     (d["msg_off"].astype(np.int64) + d["msg_sz"]).max()))
+        for f in ("sig_off", "pub_off", "msg_off"):
+            d[f] = d[f] - lo
+        parts.append(Batch(np.concatenate([adv.blob[lo:hi], np.zeros(64, np.uint8)]), d, adv.label[w * k:(w + 1) * k]))
+        if q is not None:
+            parts.append(q)
+    b = concat(parts)
+    if extra:
+        # within each window: the extras (at k..batch_sigs) move to extra_at
+        perm = np.empty(batch_sigs, np.int64)
+        rest = [i for i in range(batch_sigs) if i not in set(extra_at)]
+        perm[rest] = np.arange(k)
+        perm[extra_at] = k + np.arange(len(extra))
+        full = (np.arange(nwin)[:, None] * batch_sigs + perm[None, :]).ravel()
+        b = Batch(b.blob, b.desc[full], b.label[full])
+    return b
+

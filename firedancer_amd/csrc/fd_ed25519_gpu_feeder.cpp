@@ -214,10 +214,13 @@ static void fd_feeder_main( fd_ed25519_gpu_feeder_t * f ) {
     std::unique_lock<std::mutex> g( f->lock );
     if( f->queue.empty() && !pending ) {
       if( f->halt.load() ) break;
+      unsigned long q0 = f->queued.load( std::memory_order_acquire );
       f->sleeping.store( 1 );
       f->cv.wait_for( g, std::chrono::milliseconds( 50 ) );
       f->sleeping.store( 0 );
-      last = fd_feeder_now();
+      /* spin again only when the wait ended with work: a plain timeout of an
+         idle feeder goes straight back to sleep (no 5 ms spin per 50 ms) */
+      if( !f->queue.empty() || f->queued.load( std::memory_order_acquire ) != q0 ) last = fd_feeder_now();
     }
   }
 }

@@ -191,6 +191,7 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
   uint8_t * p = (uint8_t *)base;
   w->tab      = (int32_t *)p; p += 4UL * FD_TAB_SIG * N;
   w->pts      = (int32_t *)p; p +=  320UL * N;
+  w->fin      = (int32_t *)p; p +=  160UL * N;   /* 16-byte aligned rows: 1856 N is a multiple of 16 */
   w->status   = (int32_t *)p; p +=    4UL * N;
   w->pstat    = (int32_t *)p; p +=    8UL * N;
   w->op_start = (int32_t *)p; p +=    4UL * N;

@@ -451,6 +451,9 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
 #ifndef FD_FRONT_WAVES
 #define FD_FRONT_WAVES (FD_PREP2 ? 2 : 1)
 #endif
+#if FD_PREP2 && FD_FRONT_WAVES != 2
+#error "fd_prep2_body runs on exactly two waves per block (rounds + schedule)"
+#endif
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only (tools/front_stamps.py): histograms of the
    front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
@@ -792,6 +795,19 @@ FD_QDEV void fd_q_dblmix( fe & x, uint32_t m03, uint32_t s02 ) {
     x.v[k] = (int32_t)(((uint32_t)x.v[k] & m03) + fd_qterm( (uint32_t)b.v[k], ~0u, m03 ) + fd_qterm( (uint32_t)c.v[k], ~0u, s02 ));
 }
 
+#ifdef FD_QUAD_STAMPS
+/* diagnostic builds only (tools/quad_stamps.py): per quad-DSM wave, the
+   main loop's shader cycles (s_memtime) and 100 MHz real time
+   (s_memrealtime), summed over every launch with vector atomics:
+   [0] waves, [1] steps, [2] cycles, [3] real-time ticks, and a histogram of
+   the loop's duration per wave in 2 us bins ([8..263]) */
+__device__ unsigned long long fd_quad_acc[264];
+extern "C" hipError_t fd_ed25519_gpu_quad_acc( void * host, int clear ) {
+  if( clear ) { static unsigned long long z[264]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_quad_acc), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_quad_acc), sizeof(fd_quad_acc), 0, hipMemcpyDeviceToHost );
+}
+#endif
+
 #define FD_QSIGS 16   /* signatures per 64-lane wave */
 /* a signature's op bytes in LDS: FD_OPS_MAX + 16 (132 dwords: the 16
    rows start 4 banks apart, so the step's byte reads of 16 signatures at
@@ -929,6 +945,10 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
+#ifdef FD_QUAD_STAMPS
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   /* LITE: this signature's op byte for the next step, loaded a step ahead */
   uint8_t const * ops_i = ops + ii*FD_OPS_MAX;   /* signature-major (fd_k_front) */
   int opn = 0;
@@ -1023,6 +1043,17 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
 #endif
   }
 
+#ifdef FD_QUAD_STAMPS
+  {
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long dc = __builtin_amdgcn_s_memtime() - qs_c0, dr = __builtin_amdgcn_s_memrealtime() - qs_r0;
+    if( lane == 0u ) {
+      unsigned b = (unsigned)(dr / 200ULL); if( b > 255u ) b = 255u;
+      atomicAdd( &fd_quad_acc[0], 1ULL ); atomicAdd( &fd_quad_acc[1], (unsigned long long)(FD_OPS_MAX - t0) );
+      atomicAdd( &fd_quad_acc[2], dc ); atomicAdd( &fd_quad_acc[3], dr ); atomicAdd( &fd_quad_acc[8 + b], 1ULL );
+    }
+  }
+#endif
   /* final p1p1 -> p2: q0 X = t0 t3, q1 Y = t1 t2, q2 Z = t2 t3; then
      q0 Z r.x, q1 Z r.y and the limb compare (Q2) */
   fe P2;
@@ -1505,7 +1536,6 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   uint32_t lane = threadIdx.x & 63u;
   if( gw >= nwaves ) return;
   fd_pool_lds & L = pool[threadIdx.x >> 6];
-  uint64_t m = 2*n;
   int const EMPTY = FD_OPS_MAX << 8;
 
   /* slot init: pending signatures start at their op stream, state p1p1
@@ -1646,11 +1676,17 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       }
       nm = tn < FD_OPS_MAX ? ((tn << 8) | opn) : EMPTY;
       /* a stream that ended: its final p1p1 state out, from the slot (once
-         per signature, off the step's path) */
+         per signature, off the step's path), as the signature's own 160-byte
+         row (ten 16-byte stores; forty 4-byte stores at stride 2n wrote a
+         sector each, 1.2 KB per signature, and their 40 row offsets took 80
+         SGPRs, the kernel's spills) */
       if( tn >= FD_OPS_MAX ) {
         fe4 vf; fd_pool_ld( vf, L, s );
+        int4 * row = (int4 *)(fin + sg*40u);
 #pragma unroll
-        for( int k=0; k<40; k++ ) fin[(uint64_t)k*m + sg] = vf.l[k/10].v[k%10];
+        for( int c=0; c<10; c++ )
+          row[c] = make_int4( vf.l[(4*c)/10].v[(4*c)%10], vf.l[(4*c+1)/10].v[(4*c+1)%10],
+                              vf.l[(4*c+2)/10].v[(4*c+2)%10], vf.l[(4*c+3)/10].v[(4*c+3)%10] );
       }
     }
     fd_mem_fence();
@@ -1676,10 +1712,10 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 }
 
 /* final p1p1 -> p2 and the compare (uniform kernel's tail), one lane per
-   signature; fin holds the pool's final p1p1 states */
+   signature; fin holds the pool's final p1p1 states ([n][40] rows) */
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_dsm_final( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
-                int32_t const * __restrict__ pts, int32_t * __restrict__ out,
+                int32_t const * __restrict__ pts, int32_t const * __restrict__ fin, int32_t * __restrict__ out,
                 uint8_t const * __restrict__ blob, fd_ed25519_gpu_desc_t const * __restrict__ desc, int portable, int strict ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
@@ -1694,8 +1730,13 @@ fd_k_dsm_final( uint64_t n, int32_t const * __restrict__ status, int32_t const *
   else                                             code = FD_ST_PENDING;
   if( code != FD_ST_PENDING ) { out[i] = code; return; }
   fe4 vt;
+  int4 const * row = (int4 const *)(fin + i*40u);
 #pragma unroll
-  for( int k=0; k<40; k++ ) vt.l[k/10].v[k%10] = pts[(uint64_t)k*m + i];
+  for( int c=0; c<10; c++ ) {
+    int4 x = row[c];
+    vt.l[(4*c)/10].v[(4*c)%10] = x.x; vt.l[(4*c+1)/10].v[(4*c+1)%10] = x.y;
+    vt.l[(4*c+2)/10].v[(4*c+2)%10] = x.z; vt.l[(4*c+3)/10].v[(4*c+3)%10] = x.w;
+  }
   fe X, Y, Z;
   fd_fe_mul( X, vt.l[0], vt.l[3] );
   fd_fe_mul( Y, vt.l[1], vt.l[2] );
@@ -1834,9 +1875,9 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
        both be on the stream it runs on */
     if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     hipLaunchKernelGGL( fd_k_dsm_pool,  dim3((nw + 3u) / 4u), dim3(256), 0, stream, n, w->status, w->pstat, w->ops, w->op_start,
-                        w->tab, w->pts, portable, nw );
+                        w->tab, w->fin, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
-    hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, out, blob, desc, portable, strict );
+    hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->fin, out, blob, desc, portable, strict );
   } else if( quad ) {
     if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     if( flags & FD_ED25519_GPU_LAUNCH_DUO )

@@ -14,7 +14,9 @@
      pstat    int32 [2N]         point status, A then R
      pts      int32 [40][2N]     decompressed X,Y,Z,T limbs, A then R
      tab      int32 [N][384]     per-signature Ai table, AoS [entry 8][lane 4][12]
-                                 (10 limbs + 2 pad: 48-byte lanes, 16-byte aligned) */
+                                 (10 limbs + 2 pad: 48-byte lanes, 16-byte aligned)
+     fin      int32 [N][40]      the pooled DSM's final p1p1 states, one 160-byte row
+                                 per signature (fd_k_dsm_pool -> fd_k_dsm_final) */
 typedef struct fd_ed25519_gpu_work {
   int32_t * status;
   uint8_t * ops;
@@ -22,6 +24,7 @@ typedef struct fd_ed25519_gpu_work {
   int32_t * pstat;
   int32_t * pts;
   int32_t * tab;
+  int32_t * fin;
 } fd_ed25519_gpu_work_t;
 
 /* bytes of HBM working set per signature of capacity */
@@ -44,7 +47,7 @@ typedef struct fd_ed25519_gpu_work {
 #define FD_TAB_ENTRY (4*FD_TAB_LANE)
 #define FD_TAB_SIG   (8*FD_TAB_ENTRY)
 
-#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 4UL + (unsigned long)FD_OPS_MAX + 8UL + 320UL + 4UL*(unsigned long)FD_TAB_SIG)
+#define FD_ED25519_GPU_WORK_PER_SIG (4UL + 4UL + (unsigned long)FD_OPS_MAX + 8UL + 320UL + 160UL + 4UL*(unsigned long)FD_TAB_SIG)
 
 #ifdef __cplusplus
 extern "C" {

@@ -19,8 +19,11 @@
                      outstanding (a ring that cannot keep up is then
                      closed-loop at the window, and its latency shows it).
    Latency is push -> codes on the host (the job's t_done_ns - t_push_ns);
-   in paced mode late pushes are also reported from their scheduled time
-   (t_sched_ns) so a producer held back by a full window is not hidden. */
+   in paced mode the latency that counts is from the scheduled arrival
+   (t_sched_ns -> t_done_ns): a producer held back by a full window is
+   queueing the engine caused, and push -> done would hide it.  Every code
+   can be returned (`codes`, nbatch x batch_sigs) so the caller checks each
+   one against the reference after the timed run. */
 
 #include <stdlib.h>
 #include <string.h>
@@ -45,8 +48,12 @@ static int fd_synth_wait( fd_ed25519_gpu_job_t const * j, unsigned long bound_ns
   }
 }
 
+/* code slots are filled with this before each push: a code the engine never
+   wrote reads as 'other', not as a success left over from an earlier job */
+#define FD_SYNTH_SENTINEL 99
+
 static void fd_synth_record( fd_ed25519_gpu_synth_stat_t * st, fd_ed25519_gpu_job_t const * j, unsigned long sched,
-                             int const * out ) {
+                             int const * out, signed char * codes ) {
   st->t_sched_ns  = sched;
   st->t_push_ns   = j->t_push_ns;
   st->t_submit_ns = j->t_submit_ns;
@@ -54,10 +61,14 @@ static void fd_synth_record( fd_ed25519_gpu_synth_stat_t * st, fd_ed25519_gpu_jo
   st->t_pick_ns   = j->t_pick_ns;
   st->state       = j->state;
   for( int c=0; c<5; c++ ) st->codes[c] = 0;
-  if( j->state != 1 ) return;
+  if( j->state != 1 ) {
+    if( codes ) memset( codes, FD_SYNTH_SENTINEL, j->n );
+    return;
+  }
   for( unsigned long i=0; i<j->n; i++ ) {
     int c = out[i];
     st->codes[ c == 0 ? 0 : c == FD_ED25519_ERR_SIG ? 1 : c == FD_ED25519_ERR_PUBKEY ? 2 : c == FD_ED25519_ERR_MSG ? 3 : 4 ]++;
+    if( codes ) codes[i] = (signed char)( c >= -128 && c <= 127 ? c : FD_SYNTH_SENTINEL );
   }
 }
 
@@ -72,7 +83,8 @@ FD_EXPORT int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     f,
                                            unsigned long                 nbatch,
                                            int                           window,
                                            unsigned long                 period_ns,
-                                           fd_ed25519_gpu_synth_stat_t * stat ) {
+                                           fd_ed25519_gpu_synth_stat_t * stat,
+                                           signed char *                 codes ) {
   if( !f || !blob || !desc || !starts || !start_cnt || !stat || !batch_sigs || window < 1 || window > 64 ) return FD_ED25519_ERR_ARG;
   for( unsigned long k=0; k<start_cnt; k++ ) if( starts[k] > desc_cnt || desc_cnt - starts[k] < batch_sigs ) return FD_ED25519_ERR_ARG;
   fd_ed25519_gpu_job_t * jobs  = (fd_ed25519_gpu_job_t *)calloc( (size_t)window, sizeof(fd_ed25519_gpu_job_t) );
@@ -88,7 +100,8 @@ FD_EXPORT int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     f,
     if( i >= (unsigned long)window ) {
       fd_ed25519_gpu_job_t * j = &jobs[k];
       if( !fd_synth_wait( j, bound ) ) { err = FD_ED25519_ERR_GPU; break; }
-      fd_synth_record( &stat[i - (unsigned long)window], j, sched[k], outs + k*batch_sigs );
+      unsigned long b = i - (unsigned long)window;
+      fd_synth_record( &stat[b], j, sched[k], outs + k*batch_sigs, codes ? codes + b*batch_sigs : NULL );
       if( j->state < 0 ) err = j->state;
     }
     if( i >= nbatch ) continue;
@@ -98,6 +111,7 @@ FD_EXPORT int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     f,
     memset( j, 0, sizeof(*j) );
     j->n = batch_sigs; j->blob = blob; j->blob_sz = blob_sz;
     j->desc = desc + starts[i % start_cnt]; j->out = outs + k*batch_sigs;
+    for( unsigned long c=0; c<batch_sigs; c++ ) j->out[c] = FD_SYNTH_SENTINEL;
     sched[k] = period_ns ? when : 0UL;
     int r = fd_ed25519_gpu_feeder_push( f, j );
     if( r ) { err = r; break; }

@@ -21,10 +21,26 @@
 #include <time.h>
 #include <deque>
 #include <vector>
+#include <emmintrin.h>
 #include "fd_verify_tile.h"
 #include "fd_txn_abi.h"
 
 #define FD_EXPORT extern "C" __attribute__((visibility("default")))
+
+/* FD_VT_PROF (profiling builds only, tools/tile_host_prof.cpp): TSC cycles
+   per phase of the frag path, summed: [0] trailer check, [1] tcache,
+   [2] reserve (incl. submitting a full batch / waiting for a slot),
+   [3] frag copy, [4] descriptors + txn record, [5] publish loop (per
+   completed batch), [6] frags, [7] batches completed */
+#ifdef FD_VT_PROF
+#include <x86intrin.h>
+extern "C" { __attribute__((visibility("default"))) unsigned long fd_vt_prof[8]; }
+#define FD_VT_STAMP(v)     unsigned long v = __rdtsc()
+#define FD_VT_ACC(k,a,b)   (fd_vt_prof[k] += (b) - (a))
+#else
+#define FD_VT_STAMP(v)
+#define FD_VT_ACC(k,a,b)
+#endif
 
 /* ---- HA dedup: last `depth` distinct tags ------------------------------ */
 
@@ -137,7 +153,41 @@ struct fd_verify_tile {
   unsigned long             region_sz;
   std::vector<fd_vt_batch *> epool [ FD_VERIFY_TILE_GPU_MAX ];   /* free batches per engine */
   std::vector<fd_vt_batch *> all;
+  /* in-place mode (fd_verify_tile_new_inplace): frags are referenced where
+     they lie in the caller's registered region and DMA'd from there; a
+     batch is a span [blob, blob+used) of that region */
+  int                       inplace;
+  uint8_t const *           ip_region;
+  unsigned long             ip_region_sz;
 };
+
+/* A frag into the open batch with streaming (non-temporal) stores: the
+   batch is read next by the device's DMA, not by this thread, so its lines
+   are not pulled into the cache first (a plain memcpy reads every
+   destination line before writing it: twice the memory traffic, and the
+   tile thread's rate at C5 shape was bound by those misses,
+   profiles/r04_tile_host_prof.jsonl).  dst is 64-byte aligned (frags sit
+   on line boundaries); the last partial line is completed with zeros from
+   a staging line so every line is written whole.  fd_vt_submit fences
+   before a batch is handed to the device. */
+static void fd_vt_copy_nt( uint8_t * dst, uint8_t const * src, unsigned long sz ) {
+  unsigned long full = sz & ~63UL;
+  for( unsigned long i=0; i<full; i+=64UL ) {
+    __m128i a = _mm_loadu_si128( (__m128i const *)(src + i) );
+    __m128i b = _mm_loadu_si128( (__m128i const *)(src + i + 16UL) );
+    __m128i c = _mm_loadu_si128( (__m128i const *)(src + i + 32UL) );
+    __m128i d = _mm_loadu_si128( (__m128i const *)(src + i + 48UL) );
+    _mm_stream_si128( (__m128i *)(dst + i),        a );
+    _mm_stream_si128( (__m128i *)(dst + i + 16UL), b );
+    _mm_stream_si128( (__m128i *)(dst + i + 32UL), c );
+    _mm_stream_si128( (__m128i *)(dst + i + 48UL), d );
+  }
+  if( sz > full ) {
+    __m128i line[4] = { _mm_setzero_si128(), _mm_setzero_si128(), _mm_setzero_si128(), _mm_setzero_si128() };
+    memcpy( line, src + full, sz - full );
+    for( int k=0; k<4; k++ ) _mm_stream_si128( (__m128i *)(dst + full + 16UL*(unsigned long)k), line[k] );
+  }
+}
 
 static unsigned long fd_vt_now( void ) {
   struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
@@ -163,6 +213,7 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
     codes = t->out.data();
   }
   unsigned long tspub = fd_vt_now();
+  FD_VT_STAMP( p0 );
   for( fd_vt_txn const & x : b->txns ) {
     int ok = 1;
     for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( codes[ x.sig0 + k ] == FD_ED25519_SUCCESS );
@@ -175,6 +226,10 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
       t->diag[ FD_VERIFY_TILE_DIAG_SV_FILT_SZ  ] += x.sz;
     }
   }
+  FD_VT_STAMP( p1 ); FD_VT_ACC( 5, p0, p1 );
+#ifdef FD_VT_PROF
+  fd_vt_prof[7]++;
+#endif
   b->txns.clear(); b->ticket = 0;
   if( t->multi ) t->epool[ b->eng ].push_back( b );
   else           t->pool.push_back( b );
@@ -193,10 +248,24 @@ static int fd_vt_drain( fd_verify_tile_t * t, int block ) {
   return 0;
 }
 
+static int fd_vt_drain( fd_verify_tile_t * t, int block );
+
 static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
   if( !b || !b->nsig ) return 0;
-  if( t->multi ) {
+  _mm_sfence();   /* the batch's streaming stores are visible before the device is told */
+  if( t->inplace ) {
+    /* the span goes to the device from where it lies (a registered region:
+       no staging copy); a full ring publishes the oldest batch first */
+    for(;;) {
+      int r = fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+      if( r == 1 ) break;
+      if( r < 0 || t->inflight.empty() ) return FD_ED25519_ERR_GPU;
+      t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
+      int err = fd_vt_drain( t, 1 );
+      if( err ) return err;
+    }
+  } else if( t->multi ) {
     memset( &b->job, 0, sizeof(b->job) );
     b->job.n = b->nsig; b->job.blob = b->blob; b->job.blob_sz = b->used; b->job.desc = b->desc; b->job.out = b->codes;
     if( fd_ed25519_gpu_feeder_push( t->feeders[ b->eng ], &b->job ) ) return FD_ED25519_ERR_GPU;
@@ -208,6 +277,30 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
   t->diag[ FD_VERIFY_TILE_DIAG_BATCH_CNT ]++;
   t->inflight.push_back( b );
   t->open = NULL;
+  return 0;
+}
+
+/* in-place mode: an open batch whose span can take the frag at f (frags
+   arrive at increasing addresses until the caller's ring wraps; a frag
+   below the batch's start, or past max_blob from it, closes the batch) */
+static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsigned long nsig, unsigned long sz ) {
+  fd_vt_batch * b = t->open;
+  if( b && ( b->nsig + nsig > t->batch_sigs || f < b->blob || (unsigned long)(f - b->blob) + sz > t->max_blob ) ) {
+    int err = fd_vt_submit( t );
+    if( err ) return err;
+  }
+  while( !t->open ) {
+    if( !t->pool.empty() ) {
+      fd_vt_batch * nb = t->pool.back(); t->pool.pop_back();
+      nb->blob = (uint8_t *)f; nb->used = 0; nb->nsig = 0; nb->ticket = 0;
+      t->open = nb;
+      break;
+    }
+    if( t->inflight.empty() ) return FD_ED25519_ERR_GPU;
+    t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
+    int err = fd_vt_drain( t, 1 );
+    if( err ) return err;
+  }
   return 0;
 }
 
@@ -330,8 +423,50 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const 
   return t;
 }
 
+/* In-place mode: frags handed to rx must lie in [region, region+region_sz)
+   (e.g. the QUIC tile's dcache), which is registered with the engine here
+   and DMA'd from directly; a frag's bytes must stay unchanged until its
+   batch is published (the caller returns flow-control credits for a frag
+   after its publish, or after rx for a frag rx dropped).  Saves the tile
+   thread the frag copy: a batch's H2D reads the region itself. */
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_inplace( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
+                                                         void const * region, unsigned long region_sz,
+                                                         fd_verify_tile_publish_fn publish, void * ctx ) {
+  if( !gpu || !region || !region_sz ) return NULL;
+  fd_verify_tile_t * t = fd_verify_tile_new( gpu, cfg, publish, ctx );
+  if( !t ) return NULL;
+  if( fd_ed25519_gpu_register( gpu, (void *)region, region_sz ) ) { fd_verify_tile_delete( t ); return NULL; }
+  t->inplace = 1; t->ip_region = (uint8_t const *)region; t->ip_region_sz = region_sz;
+  /* batches own their descriptor arrays (the engine copies them into its
+     slot at submit); 2 x depth so the next batch fills while the ring is
+     full */
+  for( fd_vt_batch * b : t->pool ) delete b;
+  t->pool.clear();
+  int nb = 2 * fd_ed25519_gpu_depth( gpu );
+  for( int i=0; i<nb; i++ ) {
+    fd_vt_batch * b = new fd_vt_batch();
+    b->desc = (fd_ed25519_gpu_desc_t *)malloc( t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) );
+    b->blob = NULL; b->ticket = 0; b->used = 0; b->nsig = 0;
+    if( !b->desc ) { delete b; fd_verify_tile_delete( t ); return NULL; }
+    t->pool.push_back( b );
+    t->all.push_back( b );
+  }
+  return t;
+}
+
 FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
   if( !t ) return;
+  if( t->inplace ) {
+    while( !t->inflight.empty() ) {   /* results discarded, but the region must not be read after we return */
+      fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
+      fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
+    }
+    fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
+    for( fd_vt_batch * b : t->all ) { free( b->desc ); delete b; }
+    fd_vt_tcache_delete( t->tc );
+    delete t;
+    return;
+  }
   if( t->multi ) {
     /* feeder delete drains: every pushed job is finished (or failed after
        the engine's timeout) before the buffers go away */
@@ -359,6 +494,10 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
 FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
                                  unsigned long tsorig ) {
   uint8_t const * f = (uint8_t const *)frag;
+#ifdef FD_VT_PROF
+  fd_vt_prof[6]++;
+#endif
+  FD_VT_STAMP( s0 );
   /* trailer: [payload | pad to 2 | fd_txn_t | u16 payload_sz] */
   if( !f || sz < 2UL + sizeof(fd_txn_t) ) goto bad;
   {
@@ -375,18 +514,37 @@ FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsign
 
     unsigned long tag;
     memcpy( &tag, f + hdr.signature_off, 8 );
-    if( fd_vt_tcache_insert( t->tc, tag ) ) {
+    FD_VT_STAMP( s1 ); FD_VT_ACC( 0, s0, s1 );
+    int dup = fd_vt_tcache_insert( t->tc, tag );
+    FD_VT_STAMP( s2 ); FD_VT_ACC( 1, s1, s2 );
+    if( dup ) {
       t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;
       t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_SZ  ] += sz;
       return 0;
     }
-    unsigned long room = (sz + 7UL) & ~7UL;
-    if( room > t->max_blob ) goto bad;
-    int err = fd_vt_reserve( t, nsig, room );
-    if( err ) return err;
-    fd_vt_batch * b = t->open;
-    unsigned long base = b->used;
-    memcpy( b->blob + base, f, sz );
+    unsigned long room, base;
+    fd_vt_batch * b;
+    if( t->inplace ) {
+      /* referenced where it lies: no copy */
+      if( f < t->ip_region || sz > t->ip_region_sz || (unsigned long)(f - t->ip_region) > t->ip_region_sz - sz || sz > t->max_blob ) goto bad;
+      int err = fd_vt_reserve_inplace( t, f, nsig, sz );
+      if( err ) return err;
+      b = t->open;
+      base = (unsigned long)(f - b->blob);
+      room = base + sz > b->used ? base + sz - b->used : 0UL;   /* the span grows to the frag's end */
+      FD_VT_STAMP( s3 ); FD_VT_ACC( 2, s2, s3 );
+    } else {
+      room = (sz + 63UL) & ~63UL;   /* frags on cache-line boundaries (fd_vt_copy_nt) */
+      if( room > t->max_blob ) goto bad;
+      int err = fd_vt_reserve( t, nsig, room );
+      if( err ) return err;
+      FD_VT_STAMP( s3 ); FD_VT_ACC( 2, s2, s3 );
+      b = t->open;
+      base = b->used;
+      fd_vt_copy_nt( b->blob + base, f, sz );
+      FD_VT_STAMP( s4 ); FD_VT_ACC( 3, s3, s4 );
+    }
+    FD_VT_STAMP( s4 );
     for( unsigned long k=0; k<nsig; k++ ) {
       fd_ed25519_gpu_desc_t * d = &b->desc[ b->nsig + k ];
       d->sig_off = (uint32_t)(base + hdr.signature_off + 64UL*k);
@@ -399,6 +557,7 @@ FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsign
     b->nsig += nsig;
     b->used += room;
     t->diag[ FD_VERIFY_TILE_DIAG_SIG_CNT ] += nsig;
+    FD_VT_STAMP( s5 ); FD_VT_ACC( 4, s4, s5 );
     if( b->nsig == t->batch_sigs ) return fd_vt_submit( t );
     return 0;
   }
@@ -407,10 +566,24 @@ bad:
   return 0;
 }
 
+/* the frag path's first touches of a frag are its trailer (end) and its
+   first signature (start): in a burst they are prefetched a few frags
+   ahead, so those misses overlap the current frag's copy */
+#define FD_VT_PF 4UL
+static inline void fd_vt_prefetch( uint8_t const * base, uint64_t const * off, uint32_t const * sz, unsigned long i,
+                                   unsigned long n ) {
+  if( i + FD_VT_PF < n ) {
+    uint8_t const * f = base + off[ i + FD_VT_PF ];
+    __builtin_prefetch( f, 0, 3 );
+    __builtin_prefetch( f + sz[ i + FD_VT_PF ] - 1UL, 0, 3 );
+  }
+}
+
 FD_EXPORT int fd_verify_tile_rx_burst( fd_verify_tile_t * t, uint8_t const * base, uint64_t const * off,
                                        uint32_t const * sz, uint64_t const * ctl, uint64_t const * tsorig,
                                        unsigned long n ) {
   for( unsigned long i=0; i<n; i++ ) {
+    fd_vt_prefetch( base, off, sz, i, n );
     int err = fd_verify_tile_rx( t, base + off[i], sz[i], ctl ? ctl[i] : 0UL, tsorig ? tsorig[i] : 0UL );
     if( err ) return err;
   }
@@ -420,6 +593,7 @@ FD_EXPORT int fd_verify_tile_rx_burst( fd_verify_tile_t * t, uint8_t const * bas
 FD_EXPORT int fd_verify_tile_rx_burst_now( fd_verify_tile_t * t, uint8_t const * base, uint64_t const * off,
                                            uint32_t const * sz, unsigned long n ) {
   for( unsigned long i=0; i<n; i++ ) {
+    fd_vt_prefetch( base, off, sz, i, n );
     int err = fd_verify_tile_rx( t, base + off[i], sz[i], i, fd_vt_now() );
     if( err ) return err;
   }

@@ -72,6 +72,8 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
   if( a->device_cnt > 1 ) {
     /* one engine per device, the tile in feeder mode */
     int cnt = a->device_cnt > FD_VERIFY_TILE_GPU_MAX ? FD_VERIFY_TILE_GPU_MAX : a->device_cnt;
+    /* fini deletes gpus[0..FD_VERIFY_TILE_GPU_MAX): a caller need not zero them */
+    for( int e=0; e<FD_VERIFY_TILE_GPU_MAX; e++ ) a->gpus[e] = NULL;
     int ndev = fd_ed25519_gpu_device_cnt();
     int ok = ndev > 0;
     for( int e=0; e<cnt && ok; e++ ) {
@@ -157,7 +159,8 @@ static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
 static void fd_vt_task_fini( fd_verify_tile_args_t * a ) {
   fd_verify_tile_delete( a->tile ); a->tile = NULL;
   if( a->device_cnt > 1 ) {
-    for( int e=0; e<FD_VERIFY_TILE_GPU_MAX; e++ ) { fd_ed25519_gpu_delete( a->gpus[e] ); a->gpus[e] = NULL; }
+    int cnt = a->device_cnt > FD_VERIFY_TILE_GPU_MAX ? FD_VERIFY_TILE_GPU_MAX : a->device_cnt;
+    for( int e=0; e<cnt; e++ ) { fd_ed25519_gpu_delete( a->gpus[e] ); a->gpus[e] = NULL; }
   } else fd_ed25519_gpu_delete( a->gpu );
   a->gpu = NULL;
 }

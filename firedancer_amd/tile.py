@@ -81,8 +81,13 @@ class VerifyTile:
     lat=LatHist() records tsorig -> tspub natively instead; otherwise
     publishes are only counted."""
 
-    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True, lat=None):
+    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True, lat=None, region=None):
+        """region (a contiguous uint8 array): the in-place mode
+        (fd_verify_tile_new_inplace) -- every frag handed to rx_burst* lies
+        in it and is DMA'd from where it lies, no copy; it must stay
+        unchanged until the tile is flushed."""
         self.engine = engine
+        self._region = region
         self.published = []
         self._cb = PUBLISH_FN(self._on_publish) if collect and lat is None else None
         cfg = Cfg(batch_sigs, tcache_depth, tcache_map_cnt)
@@ -93,11 +98,12 @@ class VerifyTile:
             self._lat = lat
         if isinstance(engine, (list, tuple)):
             L = lib()
-            L.fd_verify_tile_new_multi.restype = ctypes.c_void_p
-            L.fd_verify_tile_new_multi.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p,
-                                                   ctypes.c_void_p]
             arr = (ctypes.c_void_p * len(engine))(*[e._h for e in engine])
             self._h = L.fd_verify_tile_new_multi(arr, len(engine), ctypes.byref(cfg), cb, ctx)
+        elif region is not None:
+            if region.dtype != np.uint8 or not region.flags.c_contiguous:
+                raise ValueError("region: a contiguous uint8 array")
+            self._h = lib().fd_verify_tile_new_inplace(engine._h, ctypes.byref(cfg), _p(region), region.nbytes, cb, ctx)
         else:
             self._h = lib().fd_verify_tile_new(engine._h, ctypes.byref(cfg), cb, ctx)
         if not self._h:
@@ -123,10 +129,9 @@ class VerifyTile:
 
     def rx_burst_now(self, base: np.ndarray, off: np.ndarray, sz: np.ndarray):
         """rx_burst with tsorig stamped at each frag's receipt"""
-        L = lib()
-        L.fd_verify_tile_rx_burst_now.argtypes = [ctypes.c_void_p] * 5
-        L.fd_verify_tile_rx_burst_now.restype = ctypes.c_int
-        err = L.fd_verify_tile_rx_burst_now(self._h, _p(base), _p(off), _p(sz), ctypes.c_void_p(len(off)))
+        off = np.ascontiguousarray(off, np.uint64)
+        sz = np.ascontiguousarray(sz, np.uint32)
+        err = lib().fd_verify_tile_rx_burst_now(self._h, _p(base), _p(off), _p(sz), len(off))
         if err:
             raise EngineError(f"rx_burst_now: {err}: {last_error()}")
 

@@ -429,9 +429,11 @@ int  fd_ed25519_gpu_job_wait        ( fd_ed25519_gpu_job_t const * job, long tim
    batch_sigs / period_ns), at most `window` outstanding.  stat[i] gets job
    i's stamps (t_sched_ns = its scheduled push time in paced mode, else 0),
    final state and a histogram of its codes: [0] SUCCESS, [1] ERR_SIG,
-   [2] ERR_PUBKEY, [3] ERR_MSG, [4] other.  Returns 0, FD_ED25519_ERR_ARG,
-   or the first job error (FD_ED25519_ERR_GPU if a job did not complete
-   within 30 s). */
+   [2] ERR_PUBKEY, [3] ERR_MSG, [4] other (incl. a code slot the engine
+   never wrote: each is set to 99 before its job is pushed).  codes (may be
+   NULL): nbatch x batch_sigs int8, job i's codes at codes[i*batch_sigs] (99
+   for a job that failed).  Returns 0, FD_ED25519_ERR_ARG, or the first job
+   error (FD_ED25519_ERR_GPU if a job did not complete within 30 s). */
 typedef struct fd_ed25519_gpu_synth_stat {
   unsigned long t_sched_ns, t_push_ns, t_submit_ns, t_done_ns, t_pick_ns;
   int           state;
@@ -449,7 +451,8 @@ int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     feeder,
                                  unsigned long                 nbatch,
                                  int                           window,
                                  unsigned long                 period_ns,
-                                 fd_ed25519_gpu_synth_stat_t * stat );
+                                 fd_ed25519_gpu_synth_stat_t * stat,
+                                 signed char *                 codes );
 
 /* ---- Multi-device --------------------------------
 

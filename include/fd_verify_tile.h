@@ -105,6 +105,24 @@ fd_verify_tile_new_multi( fd_ed25519_gpu_t * const *   gpus,
                           fd_verify_tile_publish_fn    publish,
                           void *                       ctx );
 
+/* In-place mode: every frag handed to rx lies in the caller's region
+   [region, region+region_sz) (e.g. the input dcache), which the tile
+   registers with the engine (fd_ed25519_gpu_register) and the engine DMAs
+   from directly: the frag path copies nothing.  A batch is the span of
+   its frags; frags arrive at increasing addresses, a lower one (the
+   caller's ring wrapped) closes the open batch.  A frag's bytes must stay
+   unchanged until it is published or dropped (the reference's flow
+   control: credits return after the frag is consumed).  NULL if the
+   region cannot be registered.  Same semantics and counters as
+   fd_verify_tile_new otherwise. */
+fd_verify_tile_t *
+fd_verify_tile_new_inplace( fd_ed25519_gpu_t *           gpu,
+                            fd_verify_tile_cfg_t const * cfg,
+                            void const *                 region,
+                            unsigned long                region_sz,
+                            fd_verify_tile_publish_fn    publish,
+                            void *                       ctx );
+
 void fd_verify_tile_delete( fd_verify_tile_t * tile );
 
 /* Receive one frag.  Returns 0 if consumed (staged, or dropped by HA

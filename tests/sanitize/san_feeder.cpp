@@ -120,13 +120,15 @@ int main( void ) {
     unsigned long starts[5] = { 0, 100, 700, 1500, ITEMS - BS };
     for( int mode=0; mode<2; mode++ ) {
       std::vector<fd_ed25519_gpu_synth_stat_t> st( NB );
+      std::vector<signed char> codes( NB*BS, 0 );
       CHECK_EQ( fd_ed25519_gpu_feeder_synth( f, blob.data(), blob_sz, all.data(), ITEMS, BS, starts, 5, NB, 3,
-                                             mode ? 200000UL : 0UL, st.data() ), 0 );
+                                             mode ? 200000UL : 0UL, st.data(), mode ? codes.data() : NULL ), 0 );
       for( unsigned long b=0; b<NB; b++ ) {
         unsigned long h[5] = { 0, 0, 0, 0, 0 };
         for( unsigned long i=0; i<BS; i++ ) {
           int c = ref[starts[b % 5] + i];
           h[ c == 0 ? 0 : c == -1 ? 1 : c == -2 ? 2 : c == -3 ? 3 : 4 ]++;
+          if( mode ) CHECK_EQ( (int)codes[b*BS + i], c );
         }
         CHECK_EQ( st[b].state, 1 );
         for( int c=0; c<5; c++ ) CHECK_EQ( st[b].codes[c], h[c] );
@@ -136,7 +138,7 @@ int main( void ) {
     }
     unsigned long bad_start[1] = { ITEMS };   /* a window past the descriptors */
     std::vector<fd_ed25519_gpu_synth_stat_t> st( 1 );
-    CHECK_EQ( fd_ed25519_gpu_feeder_synth( f, blob.data(), blob_sz, all.data(), ITEMS, BS, bad_start, 1, 1, 1, 0UL, st.data() ), FD_ED25519_ERR_ARG );
+    CHECK_EQ( fd_ed25519_gpu_feeder_synth( f, blob.data(), blob_sz, all.data(), ITEMS, BS, bad_start, 1, 1, 1, 0UL, st.data(), NULL ), FD_ED25519_ERR_ARG );
   }
 
   /* 3 (before the wedge uses up the slots). a real submit error ends its

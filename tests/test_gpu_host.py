@@ -105,12 +105,13 @@ def test_synth_producer_codes(ref, period_ns):
     e.register(base.blob)
     f = fa.Feeder(e)
     starts = np.random.default_rng(3).integers(0, len(base) - 4096, 16)
-    st = f.synth(base.blob, base.desc, 4096, starts, 48, 6, period_ns)
+    st, codes = f.synth(base.blob, base.desc, 4096, starts, 48, 6, period_ns, codes=True)
     f.close()
     e.close()
     assert (st["state"] == 1).all()
     for i in range(48):
         seg = exp[starts[i % 16]:starts[i % 16] + 4096]
+        assert (codes[i] == seg).all(), i
         want = [int((seg == 0).sum()), int((seg == -1).sum()), int((seg == -2).sum()), int((seg == -3).sum()), 0]
         assert st["codes"][i].tolist() == want, i
     assert (st["t_push_ns"] <= st["t_submit_ns"]).all() and (st["t_submit_ns"] <= st["t_done_ns"]).all()

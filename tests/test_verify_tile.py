@@ -184,3 +184,48 @@ def test_tile_multi_engine_vs_reference(ref):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch_sigs,max_blob", [(512, 4 << 20), (4096, 200_000)])
+def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob):
+    """The in-place mode (fd_verify_tile_new_inplace): frags live in one
+    registered region (the input dcache's stand-in) and each batch is DMA'd
+    from its span there, no copy.  The stream is fed in two passes over two
+    halves placed in reverse address order (the second half first), so a
+    batch also closes when the caller's ring "wraps" to a lower address, and
+    a small max_blob closes batches on span size.  Publishes and counters
+    equal the reference's per-frag semantics, in arrival order."""
+    frags = make_stream(6000, 444 + batch_sigs, ref)
+    exp_pub, exp, nsig = expected_for(frags, ref)
+    h = len(frags) // 2
+    first, second = frags[:h], frags[h:]
+    # region layout: [second half | first half]; arrival order: first, then second
+    lay = second + first
+    sz = np.array([len(f) for f in lay], np.uint32)
+    off = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
+    region = np.frombuffer(b"".join(lay) + b"\0" * 64, np.uint8).copy()
+    order = list(range(len(second), len(lay))) + list(range(len(second)))
+    e = fa.Engine(0, batch_sigs, max_blob, depth=3)
+    try:
+        tile = VerifyTile(e, batch_sigs=batch_sigs, region=region)
+        o, s_ = off[order], sz[order]
+        for a in range(0, len(order), 97):                 # bursts, with housekeeping between
+            tile.rx_burst(region, o[a:a + 97], s_[a:a + 97], ctl=np.arange(a, min(a + 97, len(order)), dtype=np.uint64))
+            tile.service()
+        tile.service(flush=True)
+        got = [(s, f) for s, f, _, _ in tile.published]
+        assert got == exp_pub
+        ctl = [c for _, _, c, _ in tile.published]
+        assert ctl == sorted(ctl)
+        d = tile.diag()
+        for k, v in exp.items():
+            assert d[k] == v, k
+        assert d["PUB_CNT"] == len(exp_pub) and d["SIG_CNT"] == nsig and d["BATCH_CNT"] >= 3
+        # a frag outside the region is malformed input, not a crash
+        other = np.frombuffer(frags[0], np.uint8).copy()
+        tile.rx_burst(other, np.zeros(1, np.uint64), np.array([len(other)], np.uint32))
+        assert tile.diag()["BAD_CNT"] == exp["BAD_CNT"] + 1
+        tile.close()
+    finally:
+        e.close()

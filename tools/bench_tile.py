@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="devices driven from this process, one tile set each")
     ap.add_argument("--multi", action="store_true",
                     help="one tile in the multi-engine feeder mode driving --tiles engines on each of --gpus devices")
+    ap.add_argument("--inplace", action="store_true",
+                    help="in-place tiles (fd_verify_tile_new_inplace): frags DMA'd from the frag set itself, no copy")
     ap.add_argument("--latency", action="store_true",
                     help="stamp tsorig at each frag's receipt and report tsorig -> tspub percentiles (native histogram)")
     ap.add_argument("--curve", default="", help="comma-separated batch sizes: one latency point per size (implies --latency)")
@@ -92,7 +94,8 @@ def run(a):
         devs = devs[:1]
     else:
         lats = [LatHist() if a.latency else None for _ in engs]
-        tiles = [VerifyTile(e, batch_sigs=a.batch, collect=False, lat=h) for e, h in zip(engs, lats)]
+        tiles = [VerifyTile(e, batch_sigs=a.batch, collect=False, lat=h, region=base if a.inplace else None)
+                 for e, h in zip(engs, lats)]
     for tile in tiles:
         tile.rx_burst(base, off, sz)            # warm-up pass
         tile.service(flush=True)
@@ -152,7 +155,7 @@ def run(a):
                           "frags_per_pass": len(frags), "sigs_per_pass": a.sigs,
                           "sig_dist": "uniform 1..12 per txn, 1232-byte txns", "pcie_inclusive": True,
                           "sv_filt_per_pass": int(d0["SV_FILT_CNT"]),
-                          "multi_engine_tile": bool(a.multi), "engines": len(engs),
+                          "multi_engine_tile": bool(a.multi), "inplace": bool(a.inplace), "engines": len(engs),
                           "latency_tsorig_to_tspub": lat_summary(lats) if a.latency else None,
                           "diag": d1}), flush=True)
     for tile in tiles:
