@@ -512,7 +512,10 @@ def latency_legs(fa, corpus, a, device):
     # (a batch the full ring holds back waits, and that wait is counted)
     paced = []
     for mps in PACED_MPS:
-        r = ring_stream(fa, ring, device, nb2, a.ring_depth, window=a.ring_depth,
+        # up to 2 x depth outstanding: the feeder always holds the next batch
+        # when a slot frees; what the ring cannot take waits in its queue
+        # and that wait is part of sched -> done
+        r = ring_stream(fa, ring, device, nb2, a.ring_depth, window=2 * a.ring_depth,
                         period_ns=int(round(BATCH_SIGS / (mps * 1e6) * 1e9)), expected=exp)
         paced.append(r)
     lat["paced"] = paced

@@ -985,8 +985,28 @@ static fd_ed25519_gpu_t * fd_default_engine( void ) {
   return fd_default_gpu;
 }
 
+/* stage() polled until a slot is free, bounded by the engine timeout */
+static int fd_stage_wait( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
+  long to = fd_timeout( g ), t0 = fd_now_ns();
+  while( fd_ed25519_gpu_stage( g, blob, desc ) ) {
+    long dt = fd_now_ns() - t0;
+    if( to >= 0 && dt > to ) {
+      snprintf( fd_gpu_err, sizeof(fd_gpu_err), "no free ring slot after %ld ms", to / 1000000L );
+      return FD_ED25519_ERR_GPU;
+    }
+    if( dt <= FD_POLL_SPIN_NS ) __builtin_ia32_pause();
+    else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
+  }
+  return 0;
+}
+
 /* Pack pointer-array inputs into a pinned slot blob in chunks of the
-   engine capacity and run them. */
+   engine capacity and run them: each chunk is staged in a free slot's
+   pinned buffers, submitted and waited on through the ring (stage /
+   try_submit / poll), so the engine lock is held only to take the slot,
+   enqueue and collect -- never across the device round trip -- and
+   callers on other threads run their batches on the other slots at the
+   same time (fd_ed25519_verify's group-commit leaders). */
 static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
                              uint8_t const * shared_msg, unsigned long shared_sz,
                              uint8_t const * const * sigp, uint8_t const (*siga)[64],
@@ -997,36 +1017,36 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
      so ERR_ARG writes nothing (fd_ed25519_gpu.h) */
   if( shared_msg ) { if( shared_sz > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG; }
   else for( unsigned long k=0; k<n; k++ ) if( msg_sz[k] > 0x7fffffffUL || msg_sz[k] > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
-  hipError_t e = hipSetDevice( g->device );
-  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
-  if( !sl ) return FD_ED25519_ERR_ARG;
   unsigned long i = 0;
   while( i < n ) {
-    /* fill one chunk */
+    void * vb; fd_ed25519_gpu_desc_t * dd;
+    int err = fd_stage_wait( g, &vb, &dd );
+    if( err ) return err;
+    uint8_t * hb = (uint8_t *)vb;
+    /* fill one chunk (the slot is ours while staged) */
     unsigned long used = 0, cnt = 0;
     unsigned long shared_off = 0;
-    if( shared_msg ) { memcpy( sl->h_blob, shared_msg, shared_sz ); used = shared_sz; }
+    if( shared_msg ) { memcpy( hb, shared_msg, shared_sz ); used = shared_sz; }
     while( i + cnt < n && cnt < g->max_sigs ) {
       unsigned long k = i + cnt;
       unsigned long msz = shared_msg ? 0UL : msg_sz[k];
       if( used + 96UL + msz > g->max_blob ) break;
-      fd_ed25519_gpu_desc_t * d = &sl->h_desc[cnt];
-      d->sig_off = (uint32_t)used; memcpy( sl->h_blob + used, sigp ? sigp[k] : siga[k], 64 ); used += 64;
-      d->pub_off = (uint32_t)used; memcpy( sl->h_blob + used, pubp ? pubp[k] : puba[k], 32 ); used += 32;
+      fd_ed25519_gpu_desc_t * d = &dd[cnt];
+      d->sig_off = (uint32_t)used; memcpy( hb + used, sigp ? sigp[k] : siga[k], 64 ); used += 64;
+      d->pub_off = (uint32_t)used; memcpy( hb + used, pubp ? pubp[k] : puba[k], 32 ); used += 32;
       if( shared_msg ) { d->msg_off = (uint32_t)shared_off; d->msg_sz = (uint32_t)shared_sz; }
       else {
         d->msg_off = (uint32_t)used; d->msg_sz = (uint32_t)msz;
-        if( msz ) memcpy( sl->h_blob + used, msg[k], msz );
+        if( msz ) memcpy( hb + used, msg[k], msz );
         used += msz;
       }
       cnt++;
     }
-    int err = fd_slot_enqueue( g, sl, cnt, sl->h_blob, used, sl->h_desc );
-    if( err ) return err;
-    if( (err = fd_event_wait( sl->done, fd_timeout( g ) )) ) { sl->ticket = g->next_ticket++; sl->orphan = 1; return err; }
-    for( unsigned long k=0; k<cnt; k++ ) out[i+k] = sl->h_out[k];
+    unsigned long ticket = 0;
+    int r = fd_ed25519_gpu_try_submit( g, cnt, hb, used, dd, &ticket );
+    if( r != 1 ) { fd_ed25519_gpu_unstage( g, hb ); return r < 0 ? r : FD_ED25519_ERR_GPU; }
+    r = fd_ed25519_gpu_poll( g, ticket, out + i, 1 );
+    if( r != 1 ) return r < 0 ? r : FD_ED25519_ERR_GPU;   /* timed out: the ticket stays valid, the slot is not reused */
     i += cnt;
   }
   return 0;
@@ -1063,18 +1083,24 @@ extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned
 
 /* fd_ed25519_verify (fd_ed25519.h:96-101): one signature per call.  Calls
    from several threads coalesce into shared batches (group commit): a call
-   joins the queue; if no batch is running it leads -- it takes every queued
-   call (up to FD_VQ_MAX) as one batch on the process-default engine, hands
-   each call its own code and wakes the rest; a call arriving while a batch
-   runs waits and rides the next one.  A lone caller waits for nothing
-   extra; N concurrent callers share one device round trip instead of
-   queueing N of them on the engine lock. */
-#define FD_VQ_MAX 4096UL
+   joins the queue; if fewer than FD_VQ_LEADERS batches are running it
+   leads -- it takes every queued call (up to FD_VQ_MAX) as one batch on
+   the process-default engine, hands each call its own code and wakes the
+   rest; a call arriving while FD_VQ_LEADERS batches run waits and rides
+   the next one.  Leaders' batches run side by side on the engine's ring
+   slots (fd_run_ptr_batch holds the engine lock only to take a slot,
+   enqueue and collect), so a call that arrives while another batch is in
+   flight does not wait a whole extra round trip behind it: with 4
+   concurrent callers and one leader at a time, every call waited for the
+   batch ahead of it (p50 0.95 ms for a 0.46 ms round trip,
+   profiles/r03_per_signature_threads.jsonl). */
+#define FD_VQ_MAX     4096UL
+#define FD_VQ_LEADERS 3        /* the default engine's ring depth (FD_GPU_DEPTH_DEFAULT) */
 struct fd_vreq { uint8_t const * m; unsigned long sz; uint8_t const * s; uint8_t const * p; int out; int done; };
 static std::mutex              fd_vq_lock;
 static std::condition_variable fd_vq_cv;
 static std::deque<fd_vreq *>   fd_vq;
-static int                     fd_vq_busy = 0;
+static int                     fd_vq_running = 0;
 
 static void fd_vq_run( std::vector<fd_vreq *> const & b, std::vector<int> & code ) {
   unsigned long n = b.size();
@@ -1099,8 +1125,9 @@ extern "C" int fd_ed25519_verify( void const * msg, unsigned long sz, void const
   std::unique_lock<std::mutex> lk( fd_vq_lock );
   fd_vq.push_back( &me );
   while( !me.done ) {
-    if( fd_vq_busy ) { fd_vq_cv.wait( lk ); continue; }
-    fd_vq_busy = 1;
+    /* lead only while this call is still queued (a leader may have taken it) */
+    if( fd_vq_running >= FD_VQ_LEADERS || fd_vq.empty() ) { fd_vq_cv.wait( lk ); continue; }
+    fd_vq_running++;
     std::vector<fd_vreq *> b;
     while( !fd_vq.empty() && b.size() < FD_VQ_MAX ) { b.push_back( fd_vq.front() ); fd_vq.pop_front(); }
     lk.unlock();
@@ -1108,7 +1135,7 @@ extern "C" int fd_ed25519_verify( void const * msg, unsigned long sz, void const
     fd_vq_run( b, code );
     lk.lock();
     for( unsigned long k=0; k<b.size(); k++ ) { b[k]->out = code[k]; b[k]->done = 1; }
-    fd_vq_busy = 0;
+    fd_vq_running--;
     fd_vq_cv.notify_all();
   }
   return me.out;

@@ -37,17 +37,6 @@ static inline unsigned long fd_synth_now( void ) {
   return (unsigned long)t.tv_sec * 1000000000UL + (unsigned long)t.tv_nsec;
 }
 
-/* busy-wait for a job (a tile polls its rings the same way), bounded */
-static int fd_synth_wait( fd_ed25519_gpu_job_t const * j, unsigned long bound_ns ) {
-  unsigned long t0 = fd_synth_now();
-  for(;;) {
-    int s = __atomic_load_n( &j->state, __ATOMIC_ACQUIRE );
-    if( s ) return s;
-    for( int k=0; k<32; k++ ) __builtin_ia32_pause();
-    if( fd_synth_now() - t0 > bound_ns ) return 0;
-  }
-}
-
 /* code slots are filled with this before each push: a code the engine never
    wrote reads as 'other', not as a success left over from an earlier job */
 #define FD_SYNTH_SENTINEL 99
@@ -90,38 +79,70 @@ FD_EXPORT int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     f,
   fd_ed25519_gpu_job_t * jobs  = (fd_ed25519_gpu_job_t *)calloc( (size_t)window, sizeof(fd_ed25519_gpu_job_t) );
   int *                  outs  = (int *)malloc( (size_t)window * batch_sigs * sizeof(int) );
   unsigned long *        sched = (unsigned long *)calloc( (size_t)window, sizeof(unsigned long) );
-  if( !jobs || !outs || !sched ) { free( jobs ); free( outs ); free( sched ); return FD_ED25519_ERR_GPU; }
+  unsigned long *        idx   = (unsigned long *)calloc( (size_t)window, sizeof(unsigned long) );   /* batch index per job slot */
+  int *                  busy  = (int *)calloc( (size_t)window, sizeof(int) );
+  int *                  fr    = (int *)calloc( (size_t)window, sizeof(int) );                     /* free job slots */
+  if( !jobs || !outs || !sched || !idx || !busy || !fr ) {
+    free( jobs ); free( outs ); free( sched ); free( idx ); free( busy ); free( fr );
+    return FD_ED25519_ERR_GPU;
+  }
+  int nfree = 0;
+  for( int k=window-1; k>=0; k-- ) fr[nfree++] = k;
   unsigned long const bound = 30000000000UL;   /* 30 s per batch: a wedged device ends the run */
   int err = 0;
+  /* every finished job is recorded and frees its slot: the ring completes
+     batches in any order (each on its own CU group), so the producer
+     refills as soon as any batch is back, not when the oldest is (a
+     producer that waited for the oldest held younger batches back behind
+     it: head-of-line blocking of its own making) */
+#define FD_SYNTH_REAP() do {                                                                           \
+    for( int k_=0; k_<window; k_++ ) {                                                                   \
+      if( !busy[k_] ) continue;                                                                          \
+      int s_ = __atomic_load_n( &jobs[k_].state, __ATOMIC_ACQUIRE );                                     \
+      if( !s_ ) continue;                                                                                \
+      fd_synth_record( &stat[idx[k_]], &jobs[k_], sched[k_], outs + (unsigned long)k_*batch_sigs,        \
+                       codes ? codes + idx[k_]*batch_sigs : NULL );                                      \
+      busy[k_] = 0; fr[nfree++] = k_;                                                                    \
+      if( s_ < 0 && !err ) err = s_;                                                                     \
+    }                                                                                                    \
+  } while(0)
   unsigned long t0 = fd_synth_now();
-  unsigned long i = 0;
-  for( ; i<nbatch + (unsigned long)window && !err; i++ ) {
-    unsigned long k = i % (unsigned long)window;
-    if( i >= (unsigned long)window ) {
-      fd_ed25519_gpu_job_t * j = &jobs[k];
-      if( !fd_synth_wait( j, bound ) ) { err = FD_ED25519_ERR_GPU; break; }
-      unsigned long b = i - (unsigned long)window;
-      fd_synth_record( &stat[b], j, sched[k], outs + k*batch_sigs, codes ? codes + b*batch_sigs : NULL );
-      if( j->state < 0 ) err = j->state;
+  for( unsigned long i=0; i<nbatch && !err; i++ ) {
+    /* a free job slot (closed loop: `window` outstanding; paced: at most) */
+    unsigned long w0 = fd_synth_now();
+    for(;;) {
+      FD_SYNTH_REAP();
+      if( nfree || err ) break;
+      if( fd_synth_now() - w0 > bound ) { err = FD_ED25519_ERR_GPU; break; }
+      for( int p=0; p<32; p++ ) __builtin_ia32_pause();
     }
-    if( i >= nbatch ) continue;
+    if( err ) break;
     unsigned long when = period_ns ? t0 + i*period_ns : 0UL;
     if( period_ns ) while( fd_synth_now() < when ) __builtin_ia32_pause();
-    fd_ed25519_gpu_job_t * j = &jobs[k];
-    memset( j, 0, sizeof(*j) );
-    j->n = batch_sigs; j->blob = blob; j->blob_sz = blob_sz;
-    j->desc = desc + starts[i % start_cnt]; j->out = outs + k*batch_sigs;
-    for( unsigned long c=0; c<batch_sigs; c++ ) j->out[c] = FD_SYNTH_SENTINEL;
+    int k = fr[--nfree];
+    fd_ed25519_gpu_job_t * jb = &jobs[k];
+    memset( jb, 0, sizeof(*jb) );
+    jb->n = batch_sigs; jb->blob = blob; jb->blob_sz = blob_sz;
+    jb->desc = desc + starts[i % start_cnt]; jb->out = outs + (unsigned long)k*batch_sigs;
+    for( unsigned long c=0; c<batch_sigs; c++ ) jb->out[c] = FD_SYNTH_SENTINEL;
     sched[k] = period_ns ? when : 0UL;
-    int r = fd_ed25519_gpu_feeder_push( f, j );
-    if( r ) { err = r; break; }
+    idx[k] = i; busy[k] = 1;
+    int r = fd_ed25519_gpu_feeder_push( f, jb );
+    if( r ) { busy[k] = 0; err = r; break; }
   }
-  if( err ) {
-    /* drain what is still outstanding before the buffers go away (each
-       wait bounded; a job never finished leaks its buffers) */
-    for( unsigned long k=0; k<(unsigned long)window; k++ )
-      if( jobs[k].n && !fd_synth_wait( &jobs[k], bound ) ) return err;
+  /* drain what is outstanding before the buffers go away (bounded; a job
+     that never finishes leaks the buffers) */
+  unsigned long w0 = fd_synth_now();
+  for(;;) {
+    FD_SYNTH_REAP();
+    int any = 0;
+    for( int k=0; k<window; k++ ) any |= busy[k];
+    if( !any ) break;
+    if( fd_synth_now() - w0 > bound ) return err ? err : FD_ED25519_ERR_GPU;
+    for( int p=0; p<32; p++ ) __builtin_ia32_pause();
   }
+#undef FD_SYNTH_REAP
+  free( idx ); free( busy ); free( fr );
   free( jobs ); free( outs ); free( sched );
   return err;
 }
