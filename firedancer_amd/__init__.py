@@ -29,8 +29,6 @@ MODE_AVX = 0        # reference AVX2 build semantics (default; SURVEY.md section
 MODE_PORTABLE = 1   # reference FD_HAS_AVX=0 build semantics
 MODE_STRICT = 2     # AVX checks with Q1-Q3 fixed (no reference build)
 
-QUAD2_NEVER, QUAD2_RING, QUAD2_ALWAYS = 0, 1, 2
-LAT_QUAD, LAT_DUO, LAT_DUO_RING = 0, 1, 2
 
 DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"), ("msg_sz", "<u4")])
 
@@ -194,14 +192,6 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_set_cu_groups.restype = ip
         L.fd_ed25519_gpu_cu_groups.argtypes = [vp]
         L.fd_ed25519_gpu_cu_groups.restype = ip
-        L.fd_ed25519_gpu_set_quad2.argtypes = [vp, ip]
-        L.fd_ed25519_gpu_set_quad2.restype = ip
-        L.fd_ed25519_gpu_quad2.argtypes = [vp]
-        L.fd_ed25519_gpu_quad2.restype = ip
-        L.fd_ed25519_gpu_set_lat_dsm.argtypes = [vp, ip]
-        L.fd_ed25519_gpu_set_lat_dsm.restype = ip
-        L.fd_ed25519_gpu_lat_dsm.argtypes = [vp]
-        L.fd_ed25519_gpu_lat_dsm.restype = ip
         L.fd_ed25519_gpu_register.argtypes = [vp, vp, ul]
         L.fd_ed25519_gpu_register.restype = ip
         L.fd_ed25519_gpu_unregister.argtypes = [vp, vp]
@@ -444,26 +434,6 @@ class Engine:
     def cu_groups(self, g: int) -> None:
         if lib().fd_ed25519_gpu_set_cu_groups(self._h, int(g)):
             raise EngineError(f"set_cu_groups({g}): ring busy or bad count")
-
-    @property
-    def quad2(self) -> int:
-        """QUAD2_NEVER / QUAD2_RING / QUAD2_ALWAYS: when small batches take the 2-waves/SIMD quad DSM"""
-        return lib().fd_ed25519_gpu_quad2(self._h)
-
-    @quad2.setter
-    def quad2(self, p: int) -> None:
-        if lib().fd_ed25519_gpu_set_quad2(self._h, int(p)):
-            raise EngineError(f"set_quad2({p})")
-
-    @property
-    def lat_dsm(self) -> int:
-        """LAT_QUAD / LAT_DUO / LAT_DUO_RING: which latency-schedule DSM small batches take"""
-        return lib().fd_ed25519_gpu_lat_dsm(self._h)
-
-    @lat_dsm.setter
-    def lat_dsm(self, p: int) -> None:
-        if lib().fd_ed25519_gpu_set_lat_dsm(self._h, int(p)):
-            raise EngineError(f"set_lat_dsm({p})")
 
     def register(self, host: np.ndarray) -> None:
         """Let the ring DMA batches straight from this (contiguous) host array."""

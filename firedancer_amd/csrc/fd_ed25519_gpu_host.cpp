@@ -142,8 +142,6 @@ struct fd_ed25519_gpu {
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
-  int           quad2;    /* FD_ED25519_GPU_QUAD2_*: when small batches take the 2-waves/SIMD quad DSM */
-  int           lat_dsm;  /* FD_ED25519_GPU_LAT_*: quad or duo DSM for small batches */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
   int           ncu;
   struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
@@ -253,12 +251,6 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );
-  /* measured slower on the ring at every depth (profiles/r02_ring_sweep_quad2.jsonl):
-     one quad wave already keeps its SIMD busy */
-  g->quad2 = FD_ED25519_GPU_QUAD2_NEVER;
-  { char const * q2 = getenv( "FD_ED25519_GPU_QUAD2" ); if( q2 ) g->quad2 = atoi( q2 ); }   /* experiments */
-  g->lat_dsm = FD_ED25519_GPU_LAT_QUAD;
-  { char const * ld = getenv( "FD_ED25519_GPU_LAT_DSM" ); if( ld ) g->lat_dsm = atoi( ld ); }   /* experiments */
   { char const * ga = getenv( "FD_ED25519_GPU_GROUP_ALWAYS" ); g->group_always = ga && atoi( ga ); }  /* experiments */
   /* a slot's pinned and device blob buffers also hold the batch's
      descriptors, 16-aligned after the padded blob, so a batch is ONE H2D
@@ -397,36 +389,14 @@ extern "C" int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * g, int groups ) 
 }
 extern "C" int fd_ed25519_gpu_cu_groups( fd_ed25519_gpu_t const * g ) { return g ? g->groups : 0; }
 
-extern "C" int fd_ed25519_gpu_set_quad2( fd_ed25519_gpu_t * g, int policy ) {
-  if( !g || policy < FD_ED25519_GPU_QUAD2_NEVER || policy > FD_ED25519_GPU_QUAD2_ALWAYS ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
-  g->quad2 = policy;
-  return 0;
-}
 /* the schedule knobs are set under the engine lock and read under it:
    submitters, the device-resident path and the feeder thread may run
    concurrently with a setter */
-struct fd_knobs { int mode; unsigned long pool_min, quad_max; int quad2, lat_dsm; };
+struct fd_knobs { int mode; unsigned long pool_min, quad_max; };
 static fd_knobs fd_knobs_get( fd_ed25519_gpu_t const * g ) {
   std::lock_guard<std::mutex> guard( const_cast<fd_ed25519_gpu_t *>( g )->lock );
-  fd_knobs k = { g->mode, g->pool_min, g->quad_max, g->quad2, g->lat_dsm };
+  fd_knobs k = { g->mode, g->pool_min, g->quad_max };
   return k;
-}
-extern "C" int fd_ed25519_gpu_quad2( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).quad2 : -1; }
-
-extern "C" int fd_ed25519_gpu_set_lat_dsm( fd_ed25519_gpu_t * g, int sched ) {
-  if( !g || sched < FD_ED25519_GPU_LAT_QUAD || sched > FD_ED25519_GPU_LAT_DUO_RING ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
-  g->lat_dsm = sched;
-  return 0;
-}
-extern "C" int fd_ed25519_gpu_lat_dsm( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).lat_dsm : -1; }
-
-/* launch flags of a batch outside the ring (device-resident paths): the
-   ring-dependent policies count as "no other batch in flight" */
-static int fd_knob_flags( fd_knobs const & kn ) {
-  return (kn.quad2 == FD_ED25519_GPU_QUAD2_ALWAYS ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0)
-       | (kn.lat_dsm == FD_ED25519_GPU_LAT_DUO ? FD_ED25519_GPU_LAUNCH_DUO : 0);
 }
 
 /* Host regions the ring may DMA from directly (no staging copy): a batch
@@ -564,7 +534,7 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   int b = (int)(g->dev_seq & 1UL);
-  int mode = kn.mode | fd_knob_flags( kn );
+  int mode = kn.mode;
   fd_ed25519_gpu_work_t const * w = &g->dev_work[b];
   hipEvent_t const * ev = NULL;
   if( g->dev_stats_on && g->dev_stats_cnt < FD_DEV_STATS_MAX ) {
@@ -674,7 +644,7 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   hipStream_t st = stream ? (hipStream_t)stream : g->slot[0].stream;
   hipError_t e0 = hipSetDevice( g->device );
   if( e0 != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e0 );
-  int mode = kn.mode | fd_knob_flags( kn );
+  int mode = kn.mode;
   if( (e0 = fd_dev_serial_begin( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   if( (e0 = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work[0], (int32_t *)d_out, st, g->kev,
                                          mode, kn.pool_min, kn.quad_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
@@ -716,11 +686,6 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   int others = sl->mstream && n <= g->mask_max && (g->group_always || busy);
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
-  /* several ring batches in flight: the quad DSM at two waves per SIMD */
-  int lflags = ( ( g->quad2 == FD_ED25519_GPU_QUAD2_ALWAYS || (g->quad2 == FD_ED25519_GPU_QUAD2_RING && busy) )
-                 ? FD_ED25519_GPU_LAUNCH_QUAD2 : 0 )
-             | ( ( g->lat_dsm == FD_ED25519_GPU_LAT_DUO || (g->lat_dsm == FD_ED25519_GPU_LAT_DUO_RING && busy) )
-                 ? FD_ED25519_GPU_LAUNCH_DUO : 0 );
   if( direct ) {
     if( (e = hipMemcpyAsync( sl->d_blob, blob, blob_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D blob (registered)", e );
@@ -729,7 +694,7 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode | lflags, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );

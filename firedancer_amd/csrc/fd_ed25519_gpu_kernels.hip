@@ -817,26 +817,11 @@ struct fd_quad_lds {
   int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
   uint8_t ops[FD_QSIGS][FD_QOPS_ROW];   /* signature-major, padded rows */
 };
-/* the two-waves-per-SIMD form: Ai lanes unpadded (40 B), nothing else in
-   LDS (op bytes and Bi come from global memory, loaded a step ahead) --
-   20 KiB per wave, 8 waves per CU */
-#define FD_QLANE 10
-struct fd_quad_lds2 {
-  int32_t tab[FD_QSIGS][8*4*FD_QLANE];
-};
-
 FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   int4 * q = (int4 *)p;
   q[0] = make_int4( v.v[0], v.v[1], v.v[2], v.v[3] );
   q[1] = make_int4( v.v[4], v.v[5], v.v[6], v.v[7] );
   q[2] = make_int4( v.v[8], v.v[9], 0, 0 );
-}
-template<int LITE> FD_QDEV void fd_q_tab_store_t( int32_t * p, fe const & v ) {
-  if constexpr( LITE ) {
-    int2 * q = (int2 *)p;
-#pragma unroll
-    for( int k=0; k<5; k++ ) q[k] = make_int2( v.v[2*k], v.v[2*k+1] );
-  } else fd_q_tab_store( p, v );
 }
 
 #ifndef FD_QUAD_ILP
@@ -856,10 +841,9 @@ template<int LITE> FD_QDEV void fd_q_tab_store_t( int32_t * p, fe const & v ) {
 #define FD_QMUL fd_fe_mul
 #endif
 
-template<int LITE, typename LDS>
 FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                            int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-                           int32_t * __restrict__ out, int strict, LDS & L ) {
+                           int32_t * __restrict__ out, int strict, fd_quad_lds & L ) {
   uint32_t lane = threadIdx.x;
   uint32_t q    = lane & 3u, ls = lane >> 2;
   uint64_t sig0 = (uint64_t)blockIdx.x * FD_QSIGS;
@@ -894,7 +878,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      independent loads per lane (a byte per lane per load, as before, was a
      ~100-deep chain of dependent round trips in front of the first step) */
   int t0 = fd_wave_min( start );
-  if constexpr( !LITE ) {
+  {
     int const c0 = t0 >> 4;
     for( int c=(int)lane; c<FD_QSIGS*(FD_OPS_MAX/16); c+=64 ) {
       int sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
@@ -914,10 +898,10 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   fe one; fd_fe_set( one, 1 );
   fe d111 = q==3u ? FD_GPU_D2 : one;
   int32_t * tab_s = L.tab[ls];
-  int const lstride = LITE ? FD_QLANE : FD_TAB_LANE, estride = 4*lstride;
+  int const lstride = FD_TAB_LANE, estride = 4*lstride;
   fe vu, vt, f, g;
   FD_QMUL( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
-  fd_q_tab_store_t<LITE>( tab_s + q*lstride, vu );
+  fd_q_tab_store( tab_s + q*lstride, vu );
   {  /* v_p2_dbl: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)), squarings as f*f, Z*(2Z) */
     fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
 #pragma unroll
@@ -936,7 +920,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
     FD_QMUL( vt, f, g );
     FD_QMUL( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
-    fd_q_tab_store_t<LITE>( tab_s + (e+1)*estride + q*lstride, vu );
+    fd_q_tab_store( tab_s + (e+1)*estride + q*lstride, vu );
   }
   __syncthreads();
 
@@ -949,38 +933,18 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  /* LITE: this signature's op byte for the next step, loaded a step ahead */
-  uint8_t const * ops_i = ops + ii*FD_OPS_MAX;   /* signature-major (fd_k_front) */
-  int opn = 0;
-  if constexpr( LITE ) opn = (t0 >= start && t0 < FD_OPS_MAX) ? (int)ops_i[t0] : 0;
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
-    int op;
-    if constexpr( LITE ) {
-      op = opn;
-      opn = (t + 1 >= start && t + 1 < FD_OPS_MAX) ? (int)ops_i[t + 1] : 0;
-    } else {
-      /* no t >= start guard: a pending signature's row is zero below its
-         op_start (its prep lane zeroed the whole row before recoding), and
-         any other row's bytes only steer lanes whose result is discarded
-         (code != FD_ST_PENDING), with table indices bounded by the masks */
-      op = (int)L.ops[ls][t];
-    }
+    /* no t >= start guard: a pending signature's row is zero below its
+       op_start (its prep lane zeroed the whole row before recoding), and
+       any other row's bytes only steer lanes whose result is discarded
+       (code != FD_ST_PENDING), with table indices bounded by the masks */
+    int op = (int)L.ops[ls][t];
     uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
     uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
     uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
     int32_t E[10];
-    if constexpr( LITE ) {
-      if( op & 0x40 ) {   /* Bi from global memory (1.5 KiB, cache resident), padded lanes */
-        int4 const * ent = (int4 const *)(fd_gpu_bi_tab + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE);
-        int4 ea = ent[0], eb = ent[1]; int2 ec = *(int2 const *)(ent + 2);
-        E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
-      } else {
-        int2 const * ent = (int2 const *)(tab_s + (op & 7)*estride + idx*lstride);
-#pragma unroll
-        for( int k=0; k<5; k++ ) { int2 x = ent[k]; E[2*k] = x.x; E[2*k+1] = x.y; }
-      }
-    } else {
+    {
       int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
       int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
@@ -1075,261 +1039,7 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
                int32_t * __restrict__ out, int strict ) {
   __shared__ __attribute__((aligned(16))) fd_quad_lds L;
-  fd_quad_body<0>( n, status, pstat, pts, ops, op_start, out, strict, L );
-}
-
-/* two waves per SIMD (streaming: several ring batches in flight) */
-extern "C" __global__ void __launch_bounds__(64, 2)
-fd_k_dsm_quad2( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
-                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-                int32_t * __restrict__ out, int strict ) {
-  __shared__ __attribute__((aligned(16))) fd_quad_lds2 L;
-  fd_quad_body<1>( n, status, pstat, pts, ops, op_start, out, strict, L );
-}
-
-/* ------------------------------------------------------------------ */
-/* Kernel 3 for the ring (4,096-signature batches under load): one lane
-   PAIR per signature ("duo"), lane a (even) carrying the reference's AVX
-   lanes 0 and 1, lane b (odd) lanes 2 and 3.  A 4-lane MUL is then two
-   independent products per lane, issued interleaved (fd_fe_mul2), and of
-   the reference's lane permutations only the pair-crossing halves cost
-   anything: one DPP swap of one field element per phase.
-
-   Why: the quad DSM spends 563 instructions per lane per step on two
-   dependent products plus its permutations and output mix (2,252 lane-
-   instructions per signature-step) and a lone quad wave stalls on its
-   serial chain (~70 % issue).  Per signature-step the duo issues ~1,800
-   lane-instructions with two independent product chains per lane, so a
-   batch costs fewer SIMD-cycles (the ring's throughput bound) at a longer
-   per-batch latency (each lane does twice the products).
-
-   The state after every step is the p1p1 point [t0,t1,t2,t3] with lane a
-   holding (t0, t1) and lane b (t2, t3).  A step (same products, same
-   operands and operand order as fd_k_dsm / fd_k_dsm_quad):
-     conversion  S = swap(t0 | t2)
-                 a: C1 = t0 t1 (T), C2 = t1 t2 (Y)
-                 b: C1 = t2 t3 (Z), C2 = t0 t3 (X)
-     op          W = swap(C2): a gets X, b gets Y
-                 a: P = (Y+X) * (D: Y+X | A: E[neg?1:2])    S = (D: X | A: T) * (D: same | A: E3)
-                 b: Q = Z * (D: 2Z | A: E0)                 R = (D: Y | A: Y-X) * (D: same | A: E[neg?2:1])
-     mix         X = swap(S | R): a gets R, b gets S
-                 a: t0 = P-R-S | P-R          t1 = R+S | P+R
-                 b: t2 = R-S | 2Q+-S           t3 = Q-R+S | 2Q-+S
-   The Ai tables live in the batch's HBM working set (fd_tab_store layout,
-   written by the wave itself) and an add step's two table lanes per lane
-   are loaded one step ahead; the op bytes come from the signature-major
-   stream two steps ahead.  No LDS, so front-end waves of the next batch
-   can share the SIMDs. */
-
-#define FD_DSIGS 32   /* signatures per 64-lane wave */
-FD_QDEV int32_t fd_dswap( int32_t x ) { return fd_qperm<FD_QP(1,0,3,2)>( x ); }
-FD_QDEV void fd_fe_dswap( fe & o, fe const & x ) {
-#pragma unroll
-  for( int k=0; k<10; k++ ) o.v[k] = fd_dswap( x.v[k] );
-}
-FD_QDEV void fd_fe_sel( fe & o, uint32_t m, fe const & a, fe const & b ) {
-#pragma unroll
-  for( int k=0; k<10; k++ ) o.v[k] = (int32_t)fd_sel( m, (uint32_t)a.v[k], (uint32_t)b.v[k] );
-}
-
-/* Setup and final stage (a few % of the work): every lane of a pair holds
-   all four AVX lanes; lane a forms products 0 and 1, lane b 2 and 3, and
-   the pair trades results. */
-FD_QDEV void fd_duo_mul4( fe4 & h, fe4 const & f, fe4 const & g, uint32_t hm ) {
-  fe fa, ga, fb, gb, ra, rb, xa, xb;
-  fd_fe_sel( fa, hm, f.l[2], f.l[0] ); fd_fe_sel( ga, hm, g.l[2], g.l[0] );
-  fd_fe_sel( fb, hm, f.l[3], f.l[1] ); fd_fe_sel( gb, hm, g.l[3], g.l[1] );
-  fd_fe_mul2( ra, fa, ga, rb, fb, gb );
-  fd_fe_dswap( xa, ra ); fd_fe_dswap( xb, rb );
-  fd_fe_sel( h.l[0], hm, xa, ra ); fd_fe_sel( h.l[1], hm, xb, rb );
-  fd_fe_sel( h.l[2], hm, ra, xa ); fd_fe_sel( h.l[3], hm, rb, xb );
-}
-
-/* one table lane (10 limbs of a 48-byte lane) */
-FD_QDEV void fd_duo_ld( fe & v, int32_t const * p ) {
-  int4 const * q = (int4 const *)p;
-  int4 a = q[0], b = q[1]; int2 c = *(int2 const *)(q + 2);
-  v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
-  v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
-  v.v[8] = c.x; v.v[9] = c.y;
-}
-
-extern "C" __global__ void __launch_bounds__(64)
-fd_k_dsm_duo( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
-              int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
-              int32_t * __restrict__ tab, int32_t * __restrict__ out, int strict ) {
-  uint32_t lane = threadIdx.x;
-  uint32_t hb   = lane & 1u;                 /* 0: lane a (AVX lanes 0,1), 1: lane b (2,3) */
-  uint32_t const hm = hb ? ~0u : 0u;
-  uint64_t i    = (uint64_t)blockIdx.x * FD_DSIGS + (lane >> 1);
-  int live = i < n;
-  uint64_t ii = live ? i : 0;
-  uint64_t m = 2*n;
-  int st = status[ii];
-  int pa = pstat[ii], pr = pstat[n+ii];
-  int code;
-  /* error precedence (fd_ed25519_user.c:372-403) */
-  if( st != FD_ST_PENDING )                        code = st;
-  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
-  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
-  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
-  else                                             code = FD_ST_PENDING;
-  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
-
-  /* vr = [Z, Y, -X, -T] of A (fd_ed25519_user.c:408-409); rr = this
-     lane's half of the final compare: a r.x, b r.y */
-  fe4 vr; fe rr;
-#pragma unroll
-  for( int k=0; k<10; k++ ) {
-    vr.l[2].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)( 0+k)*m + ii]);
-    vr.l[1].v[k] = pts[(uint64_t)(10+k)*m + ii];
-    vr.l[0].v[k] = pts[(uint64_t)(20+k)*m + ii];
-    vr.l[3].v[k] = (int32_t)(0u - (uint32_t)pts[(uint64_t)(30+k)*m + ii]);
-    rr.v[k]      = pts[(uint64_t)((hb ? 10u : 0u)+k)*m + n + ii];
-  }
-
-  /* Ai = {A,3A,...,15A} cached (avx/fd_ed25519_ge.c:423-481), the quad
-     kernel's sequence; this lane stores its two AVX lanes of each entry */
-  int32_t * tab_s = tab + ii*FD_TAB_SIG + 2u*hb*FD_TAB_LANE;
-  fe4 d111, vu, vt;
-#pragma unroll
-  for( int l=0; l<3; l++ ) fd_fe_set( d111.l[l], 1 );
-  d111.l[3] = FD_GPU_D2;
-  fd_duo_mul4( vu, vr, d111, hm ); v_subadd_12( vu );
-  if( live ) { fd_q_tab_store( tab_s, hb ? vu.l[2] : vu.l[0] ); fd_q_tab_store( tab_s + FD_TAB_LANE, hb ? vu.l[3] : vu.l[1] ); }
-  {  /* v_p2_dbl: DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)), squarings as f*f, Z*(2Z) */
-    fe4 f, g;
-    fd_fe_add( f.l[0], vr.l[2], vr.l[1] ); f.l[1] = vr.l[1]; f.l[2] = vr.l[2]; f.l[3] = vr.l[0];
-    g = f;
-#pragma unroll
-    for( int k=0; k<10; k++ ) g.l[3].v[k] = fd_twice( f.l[3].v[k] );
-    fd_duo_mul4( vt, f, g, hm );
-    v_dbl_mix( vt );
-  }
-  {
-    fe4 a, b;   /* vr = MUL(perm(vt,3,2,3,1), perm(vt,2,1,0,0)) */
-    a.l[0]=vt.l[3]; a.l[1]=vt.l[2]; a.l[2]=vt.l[3]; a.l[3]=vt.l[1];
-    b.l[0]=vt.l[2]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
-    fd_duo_mul4( vr, a, b, hm );
-  }
-  v_subadd_12( vr );
-  for( int e=0; e<7; e++ ) {
-    fd_duo_mul4( vt, vr, vu, hm );
-    v_sub_mix( vt );
-    fe4 a, b;   /* vt = MUL(perm(vt,2,3,2,1), perm(vt,3,1,0,0)) */
-    a.l[0]=vt.l[2]; a.l[1]=vt.l[3]; a.l[2]=vt.l[2]; a.l[3]=vt.l[1];
-    b.l[0]=vt.l[3]; b.l[1]=vt.l[1]; b.l[2]=vt.l[0]; b.l[3]=vt.l[0];
-    fd_duo_mul4( vt, a, b, hm );
-    fd_duo_mul4( vu, vt, d111, hm ); v_subadd_12( vu );
-    if( live ) {
-      int32_t * p = tab_s + (e+1)*FD_TAB_ENTRY;
-      fd_q_tab_store( p, hb ? vu.l[2] : vu.l[0] ); fd_q_tab_store( p + FD_TAB_LANE, hb ? vu.l[3] : vu.l[1] );
-    }
-  }
-  /* the table stores must be complete before this wave's loads of the
-     partner lane's halves below (the same wave, so no cache maintenance:
-     wait for the stores, keep the compiler from moving memory ops) */
-  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
-  __builtin_amdgcn_s_waitcnt( 0 );
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "wavefront" );
-
-  /* main loop */
-  int32_t const * tab_i = tab + ii*FD_TAB_SIG;
-  uint8_t const * ops_i = ops + ii*FD_OPS_MAX;   /* signature-major (fd_k_front) */
-  int t0 = fd_wave_min( start );
-  fe R0, R1;                                     /* a: (t0, t1), b: (t2, t3) of [0,1,1,1] */
-  fd_fe_set( R0, hb ? 1 : 0 ); fd_fe_set( R1, 1 );
-  /* rows are zero below a pending signature's op_start (its prep lane
-     zeroed the row); other rows only steer lanes whose result is
-     discarded, with table indices bounded by the masks below */
-  int op_c = t0     < FD_OPS_MAX ? (int)ops_i[t0]     : 0;
-  int op_n = t0 + 1 < FD_OPS_MAX ? (int)ops_i[t0 + 1] : 0;
-  fe EA, EB;
-#define FD_DUO_ENTRY( EA_, EB_, op_ ) do {                                                          \
-    int const o_ = (op_);                                                                           \
-    if( o_ & FD_OP_ADD ) {                                                                          \
-      uint32_t const ng_ = (uint32_t)(o_ >> 5) & 1u;                                                \
-      uint32_t const ia_ = hb ? 0u : 2u - ng_, ib_ = hb ? 1u + ng_ : 3u;                            \
-      int32_t const * en_ = ((o_ & 0x40) ? fd_gpu_bi_tab : tab_i) + (o_ & 7)*FD_TAB_ENTRY;          \
-      fd_duo_ld( EA_, en_ + ia_*FD_TAB_LANE ); fd_duo_ld( EB_, en_ + ib_*FD_TAB_LANE );             \
-    }                                                                                               \
-  } while(0)
-  FD_DUO_ENTRY( EA, EB, op_c );
-  for( int t=t0; t<FD_OPS_MAX; t++ ) {
-    int op_nn = t + 2 < FD_OPS_MAX ? (int)ops_i[t + 2] : 0;
-
-    /* conversion: a (T, Y), b (Z, X) */
-    fe C1, C2;
-    {
-      fe S, f2, g2;
-      fd_fe_dswap( S, R0 );
-      fd_fe_sel( f2, hm, S, R1 ); fd_fe_sel( g2, hm, R1, S );
-      fd_fe_mul2( C1, R0, R1, C2, f2, g2 );
-    }
-
-    /* op products: a (P, S), b (Q, R) */
-    uint32_t const add = (op_c & FD_OP_ADD) ? ~0u : 0u;
-    uint32_t const neg = ((op_c >> 5) & 1) ? ~0u : 0u;
-    fe HA, HB;
-    {
-      fe W; fd_fe_dswap( W, C2 );
-      uint32_t const aadd = ~hm & add, badd = hm & add, bdbl = hm & ~add;
-      uint32_t const bab = (uint32_t)fd_opaque( (int32_t)(badd & 1u) );
-      fe fA, gA, fB, gB;
-#pragma unroll
-      for( int k=0; k<10; k++ ) {
-        uint32_t const p0 = (uint32_t)C1.v[k], p1 = (uint32_t)C2.v[k], w = (uint32_t)W.v[k];
-        uint32_t const fa = fd_sel( hm, p0, p1 + w );
-        uint32_t const fb = fd_sel( aadd, p0, w + fd_andxor( p1, badd, badd ) + bab );
-        fA.v[k] = (int32_t)fa;
-        fB.v[k] = (int32_t)fb;
-        gA.v[k] = (int32_t)fd_sel( add, (uint32_t)EA.v[k], fa + (fa & bdbl) );
-        gB.v[k] = (int32_t)fd_sel( add, (uint32_t)EB.v[k], fb );
-      }
-      /* next step's table lanes, a step ahead of their use */
-      FD_DUO_ENTRY( EA, EB, op_n );
-      fd_fe_mul2( HA, fA, gA, HB, fB, gB );
-    }
-
-    /* output mix */
-    {
-      fe X; fd_fe_dswap( X, HB );
-      uint32_t const pos = add & ~neg;
-      uint32_t const sg  = hm & pos;             /* b, positive digit: sigma = -1 */
-      uint32_t const c0  = (~sg) & 1u, c1 = sg & 1u;
-#pragma unroll
-      for( int k=0; k<10; k++ ) {
-        uint32_t const ha = (uint32_t)HA.v[k], hbk = (uint32_t)HB.v[k], x = (uint32_t)X.v[k];
-        uint32_t const dd = ha - hbk, aa = ha + (ha & hm);
-        uint32_t const u0 = fd_sel( add, aa, fd_sel( hm, hbk, dd ) );
-        uint32_t const u1 = fd_sel( add, aa, fd_sel( hm, dd, hbk ) );
-        R0.v[k] = (int32_t)(u0 + (x ^ ~sg) + c0);
-        R1.v[k] = (int32_t)(u1 + (x ^ sg) + c1);
-      }
-    }
-    op_c = op_n; op_n = op_nn;
-  }
-#undef FD_DUO_ENTRY
-
-  /* final p1p1 -> p2 (a: X = t0 t3, b: Y = t1 t2; both Z = t2 t3), then
-     a: Z r.x vs X, b: Z r.y vs Y on limbs 0..7 (Q2) */
-  fe S0, S1, XY, Z;
-  fd_fe_dswap( S0, R0 ); fd_fe_dswap( S1, R1 );
-  {
-    fe f, g, fz, gz;
-    fd_fe_sel( f, hm, S1, R0 ); fd_fe_sel( g, hm, R0, S1 );
-    fd_fe_sel( fz, hm, R0, S0 ); fd_fe_sel( gz, hm, R1, S1 );
-    fd_fe_mul2( XY, f, g, Z, fz, gz );
-  }
-  fe cz; fd_fe_mul( cz, Z, rr );
-  int eq = 1;
-#pragma unroll
-  for( int k=0; k<8; k++ ) eq &= (cz.v[k] == XY.v[k]);
-  if( strict ) eq = fd_fe_value_eq( cz, XY );
-  int eq1 = fd_dswap( eq );
-  if( code == FD_ST_PENDING ) code = (eq & eq1) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
-  if( live && !hb ) out[i] = code;
+  fd_quad_body( n, status, pstat, pts, ops, op_start, out, strict, L );
 }
 
 /* ------------------------------------------------------------------ */
@@ -1863,7 +1573,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
                                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
                                                   hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
   if( !n ) return hipSuccess;
-  int flags = mode & ~0xff; mode &= 0xff;
+  mode &= 0xff;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
   unsigned nb  = (unsigned)((n + 255) / 256);
@@ -1880,15 +1590,8 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->fin, out, blob, desc, portable, strict );
   } else if( quad ) {
     if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
-    if( flags & FD_ED25519_GPU_LAUNCH_DUO )
-      hipLaunchKernelGGL( fd_k_dsm_duo, dim3((unsigned)((n + FD_DSIGS - 1) / FD_DSIGS)), dim3(64), 0, stream,
-                          n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out, strict );
-    else if( flags & FD_ED25519_GPU_LAUNCH_QUAD2 )
-      hipLaunchKernelGGL( fd_k_dsm_quad2, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
-                          n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
-    else
-      hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
-                          n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
+    hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
+                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
     if( ev ) hipEventRecord( ev[4], stream );
   } else {
     if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );

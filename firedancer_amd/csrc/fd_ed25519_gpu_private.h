@@ -77,12 +77,6 @@ static inline __host__ __device__ int fd_desc_in( fd_ed25519_gpu_desc_t const & 
   return (uint64_t)d.sig_off + 64UL <= blob_sz && (uint64_t)d.pub_off + 32UL <= blob_sz
       && (uint64_t)d.msg_off + (uint64_t)d.msg_sz <= blob_sz;
 }
-/* launch flag (or'd into mode): small batches take fd_k_dsm_quad2, the
-   two-waves-per-SIMD quad DSM */
-#define FD_ED25519_GPU_LAUNCH_QUAD2 (0x100)
-/* launch flag: small batches take fd_k_dsm_duo, one lane pair per
-   signature (FD_ED25519_GPU_LAT_DUO) */
-#define FD_ED25519_GPU_LAUNCH_DUO   (0x200)
 /* batches of at least this many signatures take the pooled DSM */
 #define FD_DSM_POOL_MIN_DEFAULT (262144UL)
 /* smaller batches of at most this many signatures take the quad-lane DSM */

@@ -232,33 +232,6 @@ fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );
 int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * gpu, int groups );
 int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
 
-/* Which quad-DSM form small batches take: the one-wave-per-SIMD form
-   (Ai tables, Bi and op streams in 34 KiB of LDS per wave: the lowest
-   latency for a lone batch) or the two-waves-per-SIMD form (20 KiB: more
-   throughput only where a lone wave leaves its SIMD idle).  NEVER is the
-   default: on MI355X one quad wave already keeps its SIMD busy, and the
-   second form measured slower for ring streams at every depth; RING
-   takes it while another ring batch is in flight.  Codes are identical. */
-#define FD_ED25519_GPU_QUAD2_NEVER  (0)
-#define FD_ED25519_GPU_QUAD2_RING   (1)
-#define FD_ED25519_GPU_QUAD2_ALWAYS (2)
-int fd_ed25519_gpu_set_quad2( fd_ed25519_gpu_t * gpu, int policy );
-int fd_ed25519_gpu_quad2    ( fd_ed25519_gpu_t const * gpu );
-
-/* Which latency-schedule DSM small batches (the quad path above) take:
-     FD_ED25519_GPU_LAT_QUAD: four lanes per signature (fd_k_dsm_quad),
-       the lowest latency for a lone batch;
-     FD_ED25519_GPU_LAT_DUO: one lane pair per signature (fd_k_dsm_duo),
-       fewer SIMD-cycles per batch at a longer per-batch latency;
-     FD_ED25519_GPU_LAT_DUO_RING: the duo while another ring batch is in
-       flight, the quad for a lone batch.
-   Codes are identical.  Applies to batches launched after the call. */
-#define FD_ED25519_GPU_LAT_QUAD     (0)
-#define FD_ED25519_GPU_LAT_DUO      (1)
-#define FD_ED25519_GPU_LAT_DUO_RING (2)
-int fd_ed25519_gpu_set_lat_dsm( fd_ed25519_gpu_t * gpu, int sched );
-int fd_ed25519_gpu_lat_dsm    ( fd_ed25519_gpu_t const * gpu );
-
 /* Register a host region the ring may DMA from in place
    (hipHostRegister; call before sandboxing, e.g. on the tile's input
    dcache).  A submitted blob lying inside a registered region is copied

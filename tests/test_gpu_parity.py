@@ -354,87 +354,3 @@ def test_quad_q2_vectors(engine):
     assert len(b) <= engine.dsm_quad_max
     got = engine.verify_packed(b.blob, b.desc)
     assert got.tolist() == [v["expected"] for v in vs]
-
-
-@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
-def test_quad2_golden_corpora(name):
-    """the two-waves-per-SIMD quad DSM (fd_k_dsm_quad2: unpadded Ai in LDS,
-    op bytes and Bi from global memory) gives the reference's codes"""
-    e = fa.Engine(0, 1 << 14, 1 << 24, depth=1)
-    try:
-        e.quad2 = fa.QUAD2_ALWAYS
-        b, exp = load_corpus(name)
-        got = e.verify_packed(b.blob, b.desc)
-        bad = np.nonzero(got != exp)[0]
-        assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
-    finally:
-        e.close()
-
-
-@pytest.mark.parametrize("n", [1, 15, 17, 4096 + 77, 30000])
-def test_quad2_equals_quad(engine, n):
-    base, _ = load_corpus("adversarial")
-    b = base.tile(int(np.ceil(n / len(base))))
-    b.desc = b.desc[:n]
-    e = fa.Engine(0, 1 << 15, 1 << 24, depth=1)
-    try:
-        e.quad2 = fa.QUAD2_ALWAYS
-        q2 = e.verify_packed(b.blob, b.desc)
-    finally:
-        e.close()
-    q = engine.verify_packed(b.blob, b.desc)
-    assert (q == q2).all(), np.nonzero(q != q2)[0][:10]
-
-
-@pytest.fixture(scope="module")
-def duo():
-    """an engine whose small batches run the lane-pair DSM (fd_k_dsm_duo)"""
-    e = fa.Engine(0, 1 << 15, 1 << 26, depth=1)
-    e.lat_dsm = fa.LAT_DUO
-    assert e.lat_dsm == fa.LAT_DUO
-    yield e
-    e.close()
-
-
-@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
-def test_duo_golden_corpora(duo, name):
-    """the lane-pair DSM gives the reference's codes on the golden corpora"""
-    b, exp = load_corpus(name)
-    assert len(b) <= duo.dsm_quad_max
-    got = duo.verify_packed(b.blob, b.desc)
-    bad = np.nonzero(got != exp)[0]
-    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
-
-
-def test_duo_q2_vectors(duo):
-    """the reference-quirk (Q2) and RFC 8032 vectors through the duo"""
-    vs = ed_vectors()
-    b = corpus.from_triples([(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in vs])
-    got = duo.verify_packed(b.blob, b.desc)
-    assert got.tolist() == [v["expected"] for v in vs]
-
-
-@pytest.mark.parametrize("n", [1, 31, 33, 4096 + 77, 30000])
-def test_duo_equals_quad(engine, duo, n):
-    """ragged batches (n not a multiple of the 32 signatures of a wave)"""
-    base, _ = load_corpus("adversarial")
-    b = base.tile(int(np.ceil(n / len(base))))
-    b.desc = b.desc[:n]
-    d = duo.verify_packed(b.blob, b.desc)
-    q = engine.verify_packed(b.blob, b.desc)
-    assert (q == d).all(), np.nonzero(q != d)[0][:10]
-
-
-def test_duo_c2_vs_reference(duo, ref):
-    """C2 shape (4096-signature batches of 1232-byte txns), 5% corrupted,
-    signature by signature against the reference build"""
-    b = corpus.solana_txns(4096 * 4, seed=78)
-    rng = np.random.default_rng(6)
-    for i in rng.choice(len(b), len(b) // 20, replace=False):
-        b.blob[int(b.desc[i]["sig_off"]) + rng.integers(0, 64)] ^= np.uint8(1 << rng.integers(0, 8))
-    exp = oracle_batch(ref, b)
-    for k in range(0, len(b), 4096):
-        sub = b.desc[k:k + 4096]
-        got = duo.verify_packed(b.blob, sub)
-        assert (got == exp[k:k + 4096]).all(), k
-    assert (exp != 0).sum() > 0

@@ -6,7 +6,7 @@ tail -1 gpurun_out/qops_pytest.log
 for r in 1 2 3; do FD_ED25519_LIB=$N timeout -k 10 120 python3 -u tools/time_kernels.py 4096 2> gpurun_out/tk.err || exit 1; done
 FD_ED25519_LIB=$N timeout -k 10 120 python3 -u tools/time_kernels.py 16384 2> gpurun_out/tk.err || exit 1
 FD_ED25519_LIB=$N timeout -k 10 120 python3 -u tools/time_kernels.py 32768 2> gpurun_out/tk.err || exit 1
-timeout -k 10 300 python3 -u tools/ring_sweep.py --batches 6000 --depths 8 --groups 4 --window-abs 5,6,7 --quad2 0 2>/dev/null | python3 -c "
+timeout -k 10 300 python3 -u tools/ring_sweep.py --batches 6000 --depths 8 --groups 4 --window-abs 5,6,7 2>/dev/null | python3 -c "
 import json, sys
 for l in sys.stdin:
     d = json.loads(l)
@@ -14,4 +14,4 @@ for l in sys.stdin:
 "
 O=firedancer_amd/variants/lib_old.so
 for r in 1 2; do for L in $O $N; do FD_ED25519_LIB=$L timeout -k 10 120 python3 -u tools/time_kernels.py 4096 2> gpurun_out/tk.err || exit 1; done; done
-bash tools/ab_ring.sh "--batches 4000 --depths 8 --groups 4 --window-abs 6,7 --quad2 0" $O $N || exit 1
+bash tools/ab_ring.sh "--batches 4000 --depths 8 --groups 4 --window-abs 6,7" $O $N || exit 1

@@ -12,7 +12,7 @@ echo "registered codes $V=0: $A"; echo "registered codes $V=1: $B"
 [ "$(echo $A | python3 -c 'import json,sys;print(json.load(sys.stdin)["sha256"])')" = "$(echo $B | python3 -c 'import json,sys;print(json.load(sys.stdin)["sha256"])')" ] || { echo CODES DIFFER; exit 1; }
 : > gpurun_out/ab_env.jsonl
 for R in 1 2; do for X in 0 1; do
-  env $V=$X timeout -k 10 200 python3 -u tools/ring_sweep.py --depths 8 --groups 4 --window-abs 1,6,7,8 --quad2 0 --batches 3000 > gpurun_out/ab_env.tmp 2> gpurun_out/ab_env.err || { tail -20 gpurun_out/ab_env.err; exit 1; }
+  env $V=$X timeout -k 10 200 python3 -u tools/ring_sweep.py --depths 8 --groups 4 --window-abs 1,6,7,8 --batches 3000 > gpurun_out/ab_env.tmp 2> gpurun_out/ab_env.err || { tail -20 gpurun_out/ab_env.err; exit 1; }
   python3 -c "
 import json,sys
 for l in open('gpurun_out/ab_env.tmp'):

@@ -8,7 +8,7 @@ FD_ED25519_LIB=$V timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.p
 tail -2 gpurun_out/ab_lib_pytest.log
 : > gpurun_out/ab_lib.jsonl
 for R in 1 2; do for L in $P $V; do
-  FD_ED25519_LIB=$L timeout -k 10 200 python3 -u tools/ring_sweep.py --depths 8 --groups 4 --window-abs 1,6,7,8 --quad2 0 --batches 3000 > gpurun_out/ab_lib.tmp 2> gpurun_out/ab_lib.err || { tail -20 gpurun_out/ab_lib.err; exit 1; }
+  FD_ED25519_LIB=$L timeout -k 10 200 python3 -u tools/ring_sweep.py --depths 8 --groups 4 --window-abs 1,6,7,8 --batches 3000 > gpurun_out/ab_lib.tmp 2> gpurun_out/ab_lib.err || { tail -20 gpurun_out/ab_lib.err; exit 1; }
   python3 -c "
 import json,sys
 for l in open('gpurun_out/ab_lib.tmp'):

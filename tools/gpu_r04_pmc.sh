@@ -17,7 +17,7 @@ run() {  # name driver-args counters...
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- python3 $args > $OUT/$name.txt 2>&1 || { echo "PMC $name FAILED"; tail -5 $OUT/$name.txt; return 1; }
   echo "pass $name ok"
 }
-for cfg in "quad 4096" "quad 16384" "quad2 16384" "quad2 32768"; do
+for cfg in "quad 4096" "quad 16384"; do
   set -- $cfg
   run lat_${1}_${2}_p1 "$R/tools/pmc_ring.py $1 $2" $P1 || exit 1
   run lat_${1}_${2}_p2 "$R/tools/pmc_ring.py $1 $2" $P2 || exit 1

@@ -58,7 +58,7 @@ def main():
         occ = int(v.get("Occupancy [waves/SIMD]", 0))
         alloc = (vg + 7) // 8 * 8
         by_v = VGPR_SIMD // max(alloc, 1)
-        wgw = 1 if n in ("fd_k_dsm_quad", "fd_k_dsm_quad2", "fd_k_front") else 4   # waves per workgroup
+        wgw = 1 if n in ("fd_k_dsm_quad", "fd_k_front") else 4   # waves per workgroup
         by_l = (LDS_CU // lds) * wgw // 4 if lds else WAVE_SLOTS
         limit = "+".join(x for x, y in (("VGPR", by_v), ("LDS", by_l)) if y == occ) or "waves"
         t = trace.get(n)

@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
 """Driver for PMC passes over the latency schedule's kernels (fd_k_front,
-fd_k_dsm_quad, fd_k_dsm_quad2): device-resident C2 batches of n signatures
+fd_k_dsm_quad; round 4 also ran the since-removed two-waves-per-SIMD
+fd_k_dsm_quad2, profiles/r04_pmc_ring.json): device-resident C2 batches of n signatures
 verified one at a time on a depth-1 engine (the whole device), so each
 dispatch's counters are its own (rocprofv3 --pmc serialises dispatches).
 
   n = 4096   one batch: 256 quad waves, one per SIMD on a quarter of them
   n = 16384  1,024 waves: one per SIMD on every SIMD
-  n = 32768  2,048 waves: quad2 holds two per SIMD (20 KiB of LDS each);
-             the quad (34.6 KiB) runs them in two rounds of one
+  n = 32768  2,048 waves: the quad (34.6 KiB of LDS) runs them in two
+             rounds of one per SIMD
 
-usage: pmc_ring.py <quad|quad2> <n> [reps]"""
+usage: pmc_ring.py quad <n> [reps]"""
 import math
 import os
 import sys
@@ -31,8 +32,8 @@ def main():
     b.desc = b.desc[:n]
     eng = fa.Engine(0, max_sigs=n, max_blob=max(len(b.blob), 1 << 24), depth=1)
     eng.dsm_quad_max = max(eng.dsm_quad_max, n)
-    if sched == "quad2":
-        eng.quad2 = fa.QUAD2_ALWAYS
+    if sched != "quad":
+        raise SystemExit("only the quad schedule remains (round 4)")
     dev = torch.device("cuda", 0)
     d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
     d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)

@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--windows", default="1")
     ap.add_argument("--window-abs", default="", help="comma list of absolute windows (batches in flight), instead of --windows")
     ap.add_argument("--no-register", action="store_true")
-    ap.add_argument("--quad2", default="1", help="comma list of quad2 policies (0 never, 1 ring, 2 always)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime, firedancer_amd._share_hip_runtime)
     import bench
@@ -37,9 +36,8 @@ def main():
             for w in wins:
                 if w > d:
                     continue
-                for q in [int(x) for x in a.quad2.split(",")]:
-                    r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w, register=not a.no_register, quad2=q)
-                    print(json.dumps(r), flush=True)
+                r = bench.ring_stream(fa, base, 0, a.batches, d, groups=g, window=w, register=not a.no_register)
+                print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

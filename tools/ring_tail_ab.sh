@@ -6,7 +6,7 @@ import json,sys
 d=json.loads(sys.stdin.read()); s=d.pop('slowest')
 print({k:(round(v,3) if isinstance(v,float) else v) for k,v in d.items()})" || { tail -3 gpurun_out/ring_tail.err; exit 1; }
 done; done
-timeout -k 10 300 python3 -u tools/ring_sweep.py --batches 6000 --depths 8 --groups 4 --window-abs 5,6,7 --quad2 0 2>/dev/null | python3 -c "
+timeout -k 10 300 python3 -u tools/ring_sweep.py --batches 6000 --depths 8 --groups 4 --window-abs 5,6,7 2>/dev/null | python3 -c "
 import json, sys
 for l in sys.stdin:
     d = json.loads(l)
