@@ -124,6 +124,7 @@ struct fd_vt_batch {
   uint8_t *               blob;   /* engine slot's pinned staging buffers (feeder mode: this batch's host buffers) */
   fd_ed25519_gpu_desc_t * desc;
   unsigned long           used, nsig, ticket;
+  unsigned long           first;  /* receive index of the batch's first frag */
   std::vector<fd_vt_txn>  txns;
   /* feeder mode */
   int                     eng;    /* engine (and feeder) the batch belongs to */
@@ -159,6 +160,7 @@ struct fd_verify_tile {
   int                       inplace;
   uint8_t const *           ip_region;
   unsigned long             ip_region_sz;
+  unsigned long             rx_cnt;       /* frags received (rx calls) */
 };
 
 /* A frag into the open batch with streaming (non-temporal) stores: the
@@ -491,8 +493,25 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
   delete t;
 }
 
+static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
+                                unsigned long tsorig );
+
 FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
                                  unsigned long tsorig ) {
+  int err = fd_verify_tile_rx_( t, frag, sz, ctl, tsorig );
+  t->rx_cnt++;
+  return err;
+}
+
+FD_EXPORT unsigned long fd_verify_tile_held( fd_verify_tile_t const * t ) {
+  unsigned long h = t->rx_cnt;
+  if( t->open && !t->open->txns.empty() && t->open->first < h ) h = t->open->first;
+  for( fd_vt_batch const * b : t->inflight ) if( !b->txns.empty() && b->first < h ) h = b->first;
+  return h;
+}
+
+static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
+                                unsigned long tsorig ) {
   uint8_t const * f = (uint8_t const *)frag;
 #ifdef FD_VT_PROF
   fd_vt_prof[6]++;
@@ -553,6 +572,7 @@ FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsign
       d->msg_sz  = (uint32_t)(psz - hdr.message_off);
     }
     fd_vt_txn x = { base, sz, ctl, tsorig, tag, (uint32_t)b->nsig, (uint32_t)nsig };
+    if( b->txns.empty() ) b->first = t->rx_cnt;
     b->txns.push_back( x );
     b->nsig += nsig;
     b->used += room;

@@ -84,7 +84,10 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
     a->tile = ok ? fd_verify_tile_new_multi( a->gpus, (unsigned long)cnt, &a->cfg, a->publish, a->pub_ctx ) : NULL;
   } else {
     a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, depth );
-    a->tile = a->gpu ? fd_verify_tile_new( a->gpu, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+    if( a->gpu && a->region )   /* in place: frags DMA'd from the input dcache itself */
+      a->tile = fd_verify_tile_new_inplace( a->gpu, &a->cfg, a->region, a->region_sz, a->publish, a->pub_ctx );
+    else
+      a->tile = a->gpu ? fd_verify_tile_new( a->gpu, &a->cfg, a->publish, a->pub_ctx ) : NULL;
   }
   if( !a->gpu || !a->tile ) {
     a->err = FD_ED25519_ERR_GPU;

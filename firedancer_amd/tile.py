@@ -135,6 +135,10 @@ class VerifyTile:
         if err:
             raise EngineError(f"rx_burst_now: {err}: {last_error()}")
 
+    def held(self) -> int:
+        """fd_verify_tile_held: receive index of the oldest frag still read"""
+        return int(lib().fd_verify_tile_held(self._h))
+
     def service(self, flush=False):
         err = lib().fd_verify_tile_service(self._h, 1 if flush else 0)
         if err:
@@ -181,7 +185,8 @@ class Args(ctypes.Structure):
                 ("close_fd_start", ctypes.c_uint), ("allow_syscalls_sz", ctypes.c_ushort),
                 ("allow_syscalls", ctypes.POINTER(ctypes.c_long)),
                 ("gpu", ctypes.c_void_p), ("tile", ctypes.c_void_p), ("err", ctypes.c_int),
-                ("device_cnt", ctypes.c_int), ("gpus", ctypes.c_void_p * GPU_MAX)]
+                ("device_cnt", ctypes.c_int), ("gpus", ctypes.c_void_p * GPU_MAX),
+                ("region", ctypes.c_void_p), ("region_sz", ctypes.c_ulong)]
 
 
 class TaskFns(ctypes.Structure):

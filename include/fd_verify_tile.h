@@ -173,6 +173,16 @@ void fd_verify_tile_lat_publish( void * ctx, unsigned long sig, void const * fra
    flush, also submit the partial batch and wait for all in flight. */
 int fd_verify_tile_service( fd_verify_tile_t * tile, int flush );
 
+/* Frags received so far below which the tile reads no frag any more:
+   the receive index (0-based count of rx calls) of the oldest frag an
+   open or in-flight batch may still read, or the count of frags received
+   when none.  In-place mode: the input's flow control may let the
+   producer overwrite a frag only once its receive index is below this
+   (the reference returns credits as frags are consumed; here a frag is
+   consumed when its batch is published).  Copying modes hold nothing: the
+   count of frags received. */
+unsigned long fd_verify_tile_held( fd_verify_tile_t const * tile );
+
 /* Snapshot of the diagnostic counters (FD_VERIFY_TILE_DIAG_CNT slots). */
 void fd_verify_tile_diag( fd_verify_tile_t const * tile, unsigned long * diag );
 
@@ -234,6 +244,13 @@ typedef struct {
      gpus[0..device_cnt) (gpu = gpus[0]) */
   int                        device_cnt;
   fd_ed25519_gpu_t *         gpus[ FD_VERIFY_TILE_GPU_MAX ];
+  /* in-place mode (set by the caller, single engine): region != NULL has
+     the tile read frags where they lie in [region, region+region_sz) --
+     the input dcache -- with no copy (fd_verify_tile_new_inplace); the
+     caller's input flow control then releases frags only below
+     fd_verify_tile_held( args->tile ) */
+  void const *               region;
+  unsigned long              region_sz;
 } fd_verify_tile_args_t;
 
 typedef struct {

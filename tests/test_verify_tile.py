@@ -213,7 +213,13 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob):
         for a in range(0, len(order), 97):                 # bursts, with housekeeping between
             tile.rx_burst(region, o[a:a + 97], s_[a:a + 97], ctl=np.arange(a, min(a + 97, len(order)), dtype=np.uint64))
             tile.service()
+            # nothing below the watermark is read again; an open batch holds its frags
+            h = tile.held()
+            assert h <= min(a + 97, len(order))
+            if tile.diag()["BATCH_CNT"] == 0:
+                assert h == 0
         tile.service(flush=True)
+        assert tile.held() == len(order)
         got = [(s, f) for s, f, _, _ in tile.published]
         assert got == exp_pub
         ctl = [c for _, _, c, _ in tile.published]
