@@ -146,6 +146,8 @@ def lib() -> ctypes.CDLL:
         L.fd_verify_tile_new_multi.restype = vp
         L.fd_verify_tile_new_inplace.argtypes = [vp, vp, vp, ul, vp, vp]
         L.fd_verify_tile_new_inplace.restype = vp
+        L.fd_verify_tile_new_multi_inplace.argtypes = [vp, ul, vp, vp, ul, vp, vp]
+        L.fd_verify_tile_new_multi_inplace.restype = vp
         L.fd_verify_tile_held.argtypes = [vp]
         L.fd_verify_tile_held.restype = ul
         L.fd_verify_tile_service.argtypes = [vp, ip]

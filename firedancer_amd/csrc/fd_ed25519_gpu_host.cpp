@@ -144,7 +144,7 @@ struct fd_ed25519_gpu {
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
   int           ncu;
-  struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
+  struct { uint8_t const * p; unsigned long sz; int owned; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none); atomic: set from any thread, read by waiters and feeders */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   /* device-resident path (verify_dev / _timed): its own HBM working sets,
@@ -347,7 +347,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
       snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
       return;
     }
-  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p ) hipHostUnregister( (void *)g->reg[k].p );
+  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p && g->reg[k].owned ) hipHostUnregister( (void *)g->reg[k].p );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( sl->mstream ) hipStreamDestroy( sl->mstream );
@@ -410,9 +410,15 @@ extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsig
   if( k == FD_REG_MAX ) return FD_ED25519_ERR_ARG;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  /* portable: one registration serves every device, so a region another
+     engine registered already (several engines DMAing one input dcache,
+     fd_verify_tile_new_multi_inplace) is used as is and left to that
+     engine to unregister */
   e = hipHostRegister( host, sz, hipHostRegisterPortable );
-  if( e != hipSuccess ) return fd_gpu_fail( "hipHostRegister", e );
-  g->reg[k].p = (uint8_t const *)host; g->reg[k].sz = sz;
+  int owned = 1;
+  if( e == hipErrorHostMemoryAlreadyRegistered ) { (void)hipGetLastError(); owned = 0; }
+  else if( e != hipSuccess ) return fd_gpu_fail( "hipHostRegister", e );
+  g->reg[k].p = (uint8_t const *)host; g->reg[k].sz = sz; g->reg[k].owned = owned;
   return 0;
 }
 extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
@@ -423,8 +429,8 @@ extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
       fd_ed25519_gpu_slot * sl = &g->slot[s];
       if( sl->ticket && fd_event_wait( sl->done, fd_timeout( g ) ) ) return FD_ED25519_ERR_GPU;
     }
-    hipError_t e = hipHostUnregister( host );
-    g->reg[k].p = NULL; g->reg[k].sz = 0;
+    hipError_t e = g->reg[k].owned ? hipHostUnregister( host ) : hipSuccess;
+    g->reg[k].p = NULL; g->reg[k].sz = 0; g->reg[k].owned = 0;
     return e == hipSuccess ? 0 : fd_gpu_fail( "hipHostUnregister", e );
   }
   return FD_ED25519_ERR_ARG;

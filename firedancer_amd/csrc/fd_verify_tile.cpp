@@ -256,7 +256,7 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
   if( !b || !b->nsig ) return 0;
   _mm_sfence();   /* the batch's streaming stores are visible before the device is told */
-  if( t->inplace ) {
+  if( t->inplace && !t->multi ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
     for(;;) {
@@ -292,8 +292,14 @@ static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsig
     if( err ) return err;
   }
   while( !t->open ) {
-    if( !t->pool.empty() ) {
-      fd_vt_batch * nb = t->pool.back(); t->pool.pop_back();
+    fd_vt_batch * nb = NULL;
+    if( t->multi ) {   /* a free batch of the next engine in round-robin order */
+      for( int k=0; k<t->gpu_cnt && !nb; k++ ) {
+        int e = (t->next + k) % t->gpu_cnt;
+        if( !t->epool[e].empty() ) { nb = t->epool[e].back(); t->epool[e].pop_back(); }
+      }
+    } else if( !t->pool.empty() ) { nb = t->pool.back(); t->pool.pop_back(); }
+    if( nb ) {
       nb->blob = (uint8_t *)f; nb->used = 0; nb->nsig = 0; nb->ticket = 0;
       t->open = nb;
       break;
@@ -370,9 +376,10 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
    engine owns 2 x depth batch buffers in one host allocation registered
    with it; batches go to the engines round robin and are published in
    arrival order, as with one engine. */
-FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
-                                                       fd_verify_tile_cfg_t const * cfg,
-                                                       fd_verify_tile_publish_fn publish, void * ctx ) {
+static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
+                                           fd_verify_tile_cfg_t const * cfg,
+                                           fd_verify_tile_publish_fn publish, void * ctx,
+                                           void const * ip_region, unsigned long ip_region_sz ) {
   if( !gpus || !gpu_cnt || gpu_cnt > FD_VERIFY_TILE_GPU_MAX ) return NULL;
   for( unsigned long e=0; e<gpu_cnt; e++ ) if( !gpus[e] ) return NULL;
   fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL };
@@ -391,9 +398,11 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const 
   t->gpu = gpus[0]; t->publish = publish; t->ctx = ctx; t->tc = tc;
   t->batch_sigs = c.batch_sigs; t->max_blob = maxb; t->open = NULL;
   t->multi = 1; t->gpu_cnt = (int)gpu_cnt; t->next = 0;
+  t->inplace = ip_region != NULL; t->ip_region = (uint8_t const *)ip_region; t->ip_region_sz = ip_region_sz;
   memset( t->diag, 0, sizeof(t->diag) );
-  /* per batch: blob (+64 pad, 64-aligned), descriptors, codes */
-  unsigned long blob_room = (maxb + 64UL + 63UL) & ~63UL;
+  /* per batch: blob (+64 pad, 64-aligned; none in place: a batch is a span
+     of the input region), descriptors, codes */
+  unsigned long blob_room = t->inplace ? 0UL : (maxb + 64UL + 63UL) & ~63UL;
   unsigned long per = blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL)
                     + ((c.batch_sigs * sizeof(int) + 63UL) & ~63UL);
   int ok = 1;
@@ -406,8 +415,13 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const 
     t->region[e] = (uint8_t *)r;
     memset( r, 0, t->region_sz );
     /* registered: the feeder DMAs each batch in place (no staging copy);
-       without it (no GPU-visible mapping) the feeder copies it into a slot */
-    t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], r, t->region_sz );
+       without it (no GPU-visible mapping) the feeder copies it into a slot.
+       In place it is the input region that every engine DMAs from, and a
+       tile that cannot register it is not built. */
+    if( t->inplace ) {
+      t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], (void *)ip_region, ip_region_sz );
+      if( !t->reg_ok[e] ) ok = 0;
+    } else t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], r, t->region_sz );
     for( int k=0; k<nb; k++ ) {
       fd_vt_batch * b = new fd_vt_batch();
       uint8_t * p = t->region[e] + per * (unsigned long)k;
@@ -423,6 +437,23 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const 
   }
   if( !ok ) { fd_verify_tile_delete( t ); return NULL; }
   return t;
+}
+
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
+                                                       fd_verify_tile_cfg_t const * cfg,
+                                                       fd_verify_tile_publish_fn publish, void * ctx ) {
+  return fd_vt_new_multi( gpus, gpu_cnt, cfg, publish, ctx, NULL, 0UL );
+}
+
+/* the multi-engine feeder mode in place: the input region is registered
+   with every engine and each engine's feeder DMAs its batches' spans from
+   it (fd_verify_tile_new_inplace, fd_verify_tile_new_multi) */
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_multi_inplace( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
+                                                               fd_verify_tile_cfg_t const * cfg,
+                                                               void const * region, unsigned long region_sz,
+                                                               fd_verify_tile_publish_fn publish, void * ctx ) {
+  if( !region || !region_sz ) return NULL;
+  return fd_vt_new_multi( gpus, gpu_cnt, cfg, publish, ctx, region, region_sz );
 }
 
 /* In-place mode: frags handed to rx must lie in [region, region+region_sz)
@@ -458,7 +489,7 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_inplace( fd_ed25519_gpu_t * gpu,
 
 FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
   if( !t ) return;
-  if( t->inplace ) {
+  if( t->inplace && !t->multi ) {
     while( !t->inflight.empty() ) {   /* results discarded, but the region must not be read after we return */
       fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
       fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
@@ -474,7 +505,10 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
        the engine's timeout) before the buffers go away */
     for( int e=0; e<t->gpu_cnt; e++ ) if( t->feeders[e] ) fd_ed25519_gpu_feeder_delete( t->feeders[e] );
     for( int e=0; e<t->gpu_cnt; e++ ) {
-      if( t->region[e] && t->reg_ok[e] ) fd_ed25519_gpu_unregister( t->gpus[e], t->region[e] );
+      if( t->reg_ok[e] ) {
+        if( t->inplace ) fd_ed25519_gpu_unregister( t->gpus[e], (void *)t->ip_region );
+        else if( t->region[e] ) fd_ed25519_gpu_unregister( t->gpus[e], t->region[e] );
+      }
       free( t->region[e] );
     }
     for( fd_vt_batch * b : t->all ) delete b;

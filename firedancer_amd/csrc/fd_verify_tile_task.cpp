@@ -81,7 +81,9 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
       ok = a->gpus[e] != NULL;
     }
     a->gpu  = a->gpus[0];
-    a->tile = ok ? fd_verify_tile_new_multi( a->gpus, (unsigned long)cnt, &a->cfg, a->publish, a->pub_ctx ) : NULL;
+    a->tile = !ok ? NULL
+            : a->region ? fd_verify_tile_new_multi_inplace( a->gpus, (unsigned long)cnt, &a->cfg, a->region, a->region_sz, a->publish, a->pub_ctx )
+            :             fd_verify_tile_new_multi( a->gpus, (unsigned long)cnt, &a->cfg, a->publish, a->pub_ctx );
   } else {
     a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, depth );
     if( a->gpu && a->region )   /* in place: frags DMA'd from the input dcache itself */

@@ -96,13 +96,17 @@ class VerifyTile:
         if lat is not None:                       # native latency histogram (LatHist)
             cb, ctx = lat.fn, lat.ctx
             self._lat = lat
+        if region is not None and (region.dtype != np.uint8 or not region.flags.c_contiguous):
+            raise ValueError("region: a contiguous uint8 array")
         if isinstance(engine, (list, tuple)):
             L = lib()
             arr = (ctypes.c_void_p * len(engine))(*[e._h for e in engine])
-            self._h = L.fd_verify_tile_new_multi(arr, len(engine), ctypes.byref(cfg), cb, ctx)
+            if region is not None:
+                self._h = L.fd_verify_tile_new_multi_inplace(arr, len(engine), ctypes.byref(cfg), _p(region), region.nbytes,
+                                                             cb, ctx)
+            else:
+                self._h = L.fd_verify_tile_new_multi(arr, len(engine), ctypes.byref(cfg), cb, ctx)
         elif region is not None:
-            if region.dtype != np.uint8 or not region.flags.c_contiguous:
-                raise ValueError("region: a contiguous uint8 array")
             self._h = lib().fd_verify_tile_new_inplace(engine._h, ctypes.byref(cfg), _p(region), region.nbytes, cb, ctx)
         else:
             self._h = lib().fd_verify_tile_new(engine._h, ctypes.byref(cfg), cb, ctx)

@@ -123,6 +123,18 @@ fd_verify_tile_new_inplace( fd_ed25519_gpu_t *           gpu,
                             fd_verify_tile_publish_fn    publish,
                             void *                       ctx );
 
+/* Both: the multi-engine feeder mode in place -- the region is registered
+   with every engine and each engine's feeder DMAs its batches' spans from
+   it.  NULL if any engine cannot register it. */
+fd_verify_tile_t *
+fd_verify_tile_new_multi_inplace( fd_ed25519_gpu_t * const *   gpus,
+                                  unsigned long                gpu_cnt,
+                                  fd_verify_tile_cfg_t const * cfg,
+                                  void const *                 region,
+                                  unsigned long                region_sz,
+                                  fd_verify_tile_publish_fn    publish,
+                                  void *                       ctx );
+
 void fd_verify_tile_delete( fd_verify_tile_t * tile );
 
 /* Receive one frag.  Returns 0 if consumed (staged, or dropped by HA
@@ -244,9 +256,10 @@ typedef struct {
      gpus[0..device_cnt) (gpu = gpus[0]) */
   int                        device_cnt;
   fd_ed25519_gpu_t *         gpus[ FD_VERIFY_TILE_GPU_MAX ];
-  /* in-place mode (set by the caller, single engine): region != NULL has
-     the tile read frags where they lie in [region, region+region_sz) --
-     the input dcache -- with no copy (fd_verify_tile_new_inplace); the
+  /* in-place mode (set by the caller): region != NULL has the tile read
+     frags where they lie in [region, region+region_sz) -- the input
+     dcache -- with no copy (fd_verify_tile_new_inplace, or
+     fd_verify_tile_new_multi_inplace with device_cnt > 1); the
      caller's input flow control then releases frags only below
      fd_verify_tile_held( args->tile ) */
   void const *               region;

@@ -187,15 +187,18 @@ def test_tile_multi_engine_vs_reference(ref):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch_sigs,max_blob", [(512, 4 << 20), (4096, 200_000)])
-def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob):
+@pytest.mark.parametrize("batch_sigs,max_blob,engines", [(512, 4 << 20, 1), (4096, 200_000, 1), (512, 300_000, 3)])
+def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob, engines):
     """The in-place mode (fd_verify_tile_new_inplace): frags live in one
     registered region (the input dcache's stand-in) and each batch is DMA'd
     from its span there, no copy.  The stream is fed in two passes over two
     halves placed in reverse address order (the second half first), so a
     batch also closes when the caller's ring "wraps" to a lower address, and
     a small max_blob closes batches on span size.  Publishes and counters
-    equal the reference's per-frag semantics, in arrival order."""
+    equal the reference's per-frag semantics, in arrival order.  With
+    engines > 1 the tile runs the multi-engine feeder mode in place
+    (fd_verify_tile_new_multi_inplace: the one region registered with
+    every engine, round-robin batches through their feeders)."""
     frags = make_stream(6000, 444 + batch_sigs, ref)
     exp_pub, exp, nsig = expected_for(frags, ref)
     h = len(frags) // 2
@@ -206,9 +209,9 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob):
     off = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.uint64)
     region = np.frombuffer(b"".join(lay) + b"\0" * 64, np.uint8).copy()
     order = list(range(len(second), len(lay))) + list(range(len(second)))
-    e = fa.Engine(0, batch_sigs, max_blob, depth=3)
+    es = [fa.Engine(0, batch_sigs, max_blob, depth=3 if engines == 1 else 2) for _ in range(engines)]
     try:
-        tile = VerifyTile(e, batch_sigs=batch_sigs, region=region)
+        tile = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region)
         o, s_ = off[order], sz[order]
         for a in range(0, len(order), 97):                 # bursts, with housekeeping between
             tile.rx_burst(region, o[a:a + 97], s_[a:a + 97], ctl=np.arange(a, min(a + 97, len(order)), dtype=np.uint64))
@@ -234,4 +237,5 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob):
         assert tile.diag()["BAD_CNT"] == exp["BAD_CNT"] + 1
         tile.close()
     finally:
-        e.close()
+        for e in es:
+            e.close()

@@ -90,7 +90,7 @@ def run(a):
     from firedancer_amd.tile import LatHist
     if a.multi:       # one tile, every engine behind its feeder
         lats = [LatHist()] if a.latency else [None]
-        tiles = [VerifyTile(engs, batch_sigs=a.batch, collect=False, lat=lats[0])]
+        tiles = [VerifyTile(engs, batch_sigs=a.batch, collect=False, lat=lats[0], region=base if a.inplace else None)]
         devs = devs[:1]
     else:
         lats = [LatHist() if a.latency else None for _ in engs]
