@@ -24,6 +24,7 @@
 #include <condition_variable>
 #include <vector>
 #include <atomic>
+#include <map>
 #include "fd_ed25519_gpu_private.h"
 
 #define FD_GPU_DEPTH_DEFAULT 3
@@ -144,7 +145,7 @@ struct fd_ed25519_gpu {
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
   int           ncu;
-  struct { uint8_t const * p; unsigned long sz; int owned; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
+  struct { uint8_t const * p; unsigned long sz; } reg[FD_REG_MAX];   /* hipHostRegister'ed source regions */
   long          timeout_ns; /* bound on one blocking wait (< 0: none); atomic: set from any thread, read by waiters and feeders */
   fd_ed25519_gpu_slot slot[FD_GPU_DEPTH_MAX];
   /* device-resident path (verify_dev / _timed): its own HBM working sets,
@@ -327,6 +328,8 @@ static int fd_stream_query( void * st ) {
   return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -1;
 }
 
+static hipError_t fd_reg_release( void * host );
+
 extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   if( !g ) return;
   hipSetDevice( g->device );
@@ -347,7 +350,7 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
       snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
       return;
     }
-  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p && g->reg[k].owned ) hipHostUnregister( (void *)g->reg[k].p );
+  for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p ) fd_reg_release( (void *)g->reg[k].p );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( sl->mstream ) hipStreamDestroy( sl->mstream );
@@ -401,7 +404,38 @@ static fd_knobs fd_knobs_get( fd_ed25519_gpu_t const * g ) {
 
 /* Host regions the ring may DMA from directly (no staging copy): a batch
    whose blob lies inside one goes H2D straight from the caller's bytes
-   (plus the descriptors from the slot's pinned buffer). */
+   (plus the descriptors from the slot's pinned buffer).  Registrations are
+   process-wide and counted: several engines may register one region (one
+   input dcache DMA'd by every engine of a multi-engine tile in place,
+   fd_verify_tile_new_multi_inplace); the runtime registers it once
+   (portable: every device) and unregisters it with the last engine. */
+static std::mutex                                                      fd_reg_lock;
+static std::map<void const *, std::pair<unsigned long, unsigned long>> fd_reg_cnt;   /* host -> (sz, engines) */
+
+static hipError_t fd_reg_acquire( void * host, unsigned long sz ) {
+  std::lock_guard<std::mutex> guard( fd_reg_lock );
+  auto it = fd_reg_cnt.find( host );
+  if( it != fd_reg_cnt.end() ) {
+    if( it->second.first != sz ) return hipErrorInvalidValue;   /* the same start, another size: not shareable */
+    it->second.second++;
+    return hipSuccess;
+  }
+  hipError_t e = hipHostRegister( host, sz, hipHostRegisterPortable );
+  if( e != hipSuccess ) { (void)hipGetLastError(); return e; }
+  fd_reg_cnt[ host ] = std::make_pair( sz, 1UL );
+  return hipSuccess;
+}
+static hipError_t fd_reg_release( void * host ) {
+  std::lock_guard<std::mutex> guard( fd_reg_lock );
+  auto it = fd_reg_cnt.find( host );
+  if( it == fd_reg_cnt.end() ) return hipErrorHostMemoryNotRegistered;
+  if( --it->second.second ) return hipSuccess;
+  fd_reg_cnt.erase( it );
+  hipError_t e = hipHostUnregister( host );
+  if( e != hipSuccess ) (void)hipGetLastError();
+  return e;
+}
+
 extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsigned long sz ) {
   if( !g || !host || !sz ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
@@ -410,15 +444,9 @@ extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsig
   if( k == FD_REG_MAX ) return FD_ED25519_ERR_ARG;
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
-  /* portable: one registration serves every device, so a region another
-     engine registered already (several engines DMAing one input dcache,
-     fd_verify_tile_new_multi_inplace) is used as is and left to that
-     engine to unregister */
-  e = hipHostRegister( host, sz, hipHostRegisterPortable );
-  int owned = 1;
-  if( e == hipErrorHostMemoryAlreadyRegistered ) { (void)hipGetLastError(); owned = 0; }
-  else if( e != hipSuccess ) return fd_gpu_fail( "hipHostRegister", e );
-  g->reg[k].p = (uint8_t const *)host; g->reg[k].sz = sz; g->reg[k].owned = owned;
+  e = fd_reg_acquire( host, sz );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipHostRegister", e );
+  g->reg[k].p = (uint8_t const *)host; g->reg[k].sz = sz;
   return 0;
 }
 extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
@@ -429,8 +457,8 @@ extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
       fd_ed25519_gpu_slot * sl = &g->slot[s];
       if( sl->ticket && fd_event_wait( sl->done, fd_timeout( g ) ) ) return FD_ED25519_ERR_GPU;
     }
-    hipError_t e = g->reg[k].owned ? hipHostUnregister( host ) : hipSuccess;
-    g->reg[k].p = NULL; g->reg[k].sz = 0; g->reg[k].owned = 0;
+    hipError_t e = fd_reg_release( host );
+    g->reg[k].p = NULL; g->reg[k].sz = 0;
     return e == hipSuccess ? 0 : fd_gpu_fail( "hipHostUnregister", e );
   }
   return FD_ED25519_ERR_ARG;
