@@ -88,7 +88,8 @@ SLOTS_DECOMP = 2 * (264 * SLOT_SQ + 3 * SLOT_SQ2 + 32 * SLOT_MUL + 60 + 120)
 # fd_k_prep: SHA-512 blocks + S check, sc_reduce (~600) and two wNAF-5
 #   recodings (~1,700 each) = 4,000 fixed.
 SLOTS_PREP_FIXED = 4000
-PEAK_INT32_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T slots/s
+PEAK_CLOCK_GHZ = 2.4
+PEAK_INT32_OPS = 256 * 4 * 32 * PEAK_CLOCK_GHZ * 1e9   # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T slots/s
 
 
 def sha_blocks(msg_sz):
@@ -367,9 +368,13 @@ def main():
     hist = codes_hist(d_out.cpu().numpy())
     ok = valid_corpus_ok(hist, n_step)
     solo = rank == 0 and world == 1
+    def on_start():
+        eng.dev_stats_begin()
+        eng.dsm_clock(clear=True)
     elapsed = timed_region(step, a.steps, max(a.warmup - 1, 0), dist, red_dev, torch.cuda.synchronize,
-                           on_start=eng.dev_stats_begin if solo else None)
+                           on_start=on_start if solo else None)
     live = eng.dev_stats_end() if solo else None
+    clock = eng.dsm_clock() if solo else None
     ok = all_ranks_ok(ok, dist, red_dev)
     res = result_line(a, world, n_step, elapsed, ok, base, hist)
     value = res["value"]
@@ -421,6 +426,15 @@ def main():
             "traffic": traffic,
             "per_kernel": kern,
             "pipeline_frac": value * w_total / PEAK_INT32_OPS,
+            # the shader clock the pool ran at over the timed launches (s_memtime vs
+            # the 100 MHz s_memrealtime, summed over its waves): the peak assumes
+            # 2.4 GHz, so boxes whose DVFS holds a lower clock under this load
+            # read a lower frac for the same code
+            "effective_clock_ghz": clock["pool"]["ghz"],
+            "frac_at_effective_clock": (kern[dom]["frac"] * PEAK_CLOCK_GHZ / clock["pool"]["ghz"]
+                                        if clock["pool"]["ghz"] else None),
+            "clock_source": "fd_ed25519_gpu_dsm_clock: fd_k_dsm_pool waves' s_memtime / s_memrealtime "
+                            f"over the timed launches ({clock['pool']['waves']} waves)",
             "ops_per_verify": w_total,
             "kernel_ms_source": f"HIP events around each kernel on its stream over {timed_launches} timed launches "
                                 "(pipelined: launch k's front end overlaps launch k-1's DSM); ms_serial: each "
@@ -433,8 +447,13 @@ def main():
                             "VALU-bound, traffic is a secondary check",
         }
         if not a.no_latency:
+            eng.dsm_clock(clear=True)
             res["latency"] = latency_legs(fa, corpus, a, local)
             lat = res["latency"]
+            torch.cuda.synchronize()
+            qc = eng.dsm_clock()["quad"]
+            lat["dsm_quad_effective_clock_ghz"] = qc["ghz"]
+            lat["dsm_quad_clock_waves"] = qc["waves"]
             res["ring_4096_verifies_per_s"] = lat["pcie_inclusive_verifies_per_s"]
             res["ring_4096_best_verifies_per_s_at_p99_le_1ms"] = (lat["best_under_p99_1ms"] or {}).get("verifies_per_s")
             res["ring_4096_max_offered_at_sched_p99_le_1ms"] = lat["max_offered_at_sched_p99_le_1ms"]

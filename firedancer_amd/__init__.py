@@ -88,6 +88,8 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_dev_stats_begin.restype = ip
         L.fd_ed25519_gpu_dev_stats_end.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fd_ed25519_gpu_dev_stats_end.restype = ip
+        L.fd_ed25519_gpu_dsm_clock.argtypes = [vp, ip, vp]
+        L.fd_ed25519_gpu_dsm_clock.restype = ip
         L.fd_ed25519_gpu_kernel_cnt.argtypes = []
         L.fd_ed25519_gpu_kernel_cnt.restype = ip
         L.fd_ed25519_public_batch.argtypes = [ul, vp, vp, ip]
@@ -313,6 +315,21 @@ class Engine:
         if err:
             raise EngineError(f"dev_stats_end: {strerror(err)}: {last_error()}")
         return (ms / max(cnt.value, 1)).astype(np.float64), cnt.value
+
+    def dsm_clock(self, clear: bool = False):
+        """Shader clock the DSM kernels ran at on this engine's device since
+        the last clear (fd_ed25519_gpu_dsm_clock): None after clear=True,
+        else {"pool": {"waves", "ghz"}, "quad": {...}} (ghz None when no wave
+        of that kernel ran).  Call with the device idle."""
+        out = np.zeros(6, np.uint64)
+        err = lib().fd_ed25519_gpu_dsm_clock(self._h, 1 if clear else 0, None if clear else _p(out))
+        if err:
+            raise EngineError(f"dsm_clock: {strerror(err)}: {last_error()}")
+        if clear:
+            return None
+        def one(w, c, t):
+            return {"waves": int(w), "ghz": (0.1 * float(c) / float(t)) if t else None}
+        return {"pool": one(*out[0:3]), "quad": one(*out[3:6])}
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
         """Queue a batch on the pinned ring; returns its ticket."""

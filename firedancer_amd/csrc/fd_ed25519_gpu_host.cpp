@@ -636,6 +636,17 @@ extern "C" int fd_ed25519_gpu_dev_stats_end( fd_ed25519_gpu_t * g, float * kerne
   return 0;
 }
 
+/* the DSM kernels' clock accumulators (fd_dsm_clk, kernels.hip): clear, or
+   read [pool waves, cycles, ticks, quad waves, cycles, ticks] */
+extern "C" hipError_t fd_ed25519_gpu_dsm_clk_xfer( unsigned long long * host, int clear );
+extern "C" int fd_ed25519_gpu_dsm_clock( fd_ed25519_gpu_t * g, int clear, unsigned long long * out ) {
+  if( !g || (!clear && !out) ) return FD_ED25519_ERR_ARG;
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
+  if( (e = fd_ed25519_gpu_dsm_clk_xfer( out, clear )) != hipSuccess ) return fd_gpu_fail( "dsm clock", e );
+  return 0;
+}
+
 /* a serial device-resident operation on `st` using working set 0: waits
    for every earlier pipelined launch, and later ones wait for it */
 static hipError_t fd_dev_serial_begin( fd_ed25519_gpu_t * g, hipStream_t st ) {

@@ -49,6 +49,28 @@ __device__ static int32_t fd_gpu_bi_tab[8*FD_TAB_ENTRY];
 #define FD_DSM_WAVES 2
 #endif
 
+/* Shader clock under the DSM kernels: per wave, the main loop's shader
+   cycles (s_memtime) and 100 MHz real-time ticks (s_memrealtime), summed
+   with one vector atomic each from lane 0 (a few per 1,000 signatures):
+   [0] waves, [1] cycles, [2] ticks of fd_k_dsm_pool; [3..5] the same for
+   fd_k_dsm_quad.  cycles / ticks x 0.1 GHz is the clock the kernel ran at,
+   which separates a box's DVFS state from a code regression in the
+   bench's roofline (fd_ed25519_gpu_dsm_clock). */
+__device__ unsigned long long fd_dsm_clk[6];
+extern "C" hipError_t fd_ed25519_gpu_dsm_clk_xfer( unsigned long long * host, int clear ) {
+  if( clear ) { static unsigned long long const z[6] = { 0, 0, 0, 0, 0, 0 }; return hipMemcpyToSymbol( HIP_SYMBOL(fd_dsm_clk), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_dsm_clk), sizeof(fd_dsm_clk), 0, hipMemcpyDeviceToHost );
+}
+FD_DEV void fd_clk_add( int k, unsigned long long c0, unsigned long long r0, uint32_t lane ) {
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long dc = __builtin_amdgcn_s_memtime() - c0, dr = __builtin_amdgcn_s_memrealtime() - r0;
+  if( lane == 0u ) {
+    __hip_atomic_fetch_add( &fd_dsm_clk[k+0], 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    __hip_atomic_fetch_add( &fd_dsm_clk[k+1], dc,   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    __hip_atomic_fetch_add( &fd_dsm_clk[k+2], dr,   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  }
+}
+
 /* ------------------------------------------------------------------ */
 /* 4-lane vector helpers: the AVX path's wl_t x 10 state, one field
    element per lane (fd_ed25519_fe_avx.h:32-69). */
@@ -929,10 +951,8 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
-#ifdef FD_QUAD_STAMPS
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
     /* no t >= start guard: a pending signature's row is zero below its
        op_start (its prep lane zeroed the whole row before recoding), and
@@ -1018,6 +1038,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     }
   }
 #endif
+  fd_clk_add( 3, qs_c0, qs_r0, lane );
   /* final p1p1 -> p2: q0 X = t0 t3, q1 Y = t1 t2, q2 Z = t2 t3; then
      q0 Z r.x, q1 Z r.y and the limb compare (Q2) */
   fe P2;
@@ -1272,6 +1293,8 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
   fd_mem_fence();
 
   int lo_d = 0, lo_a = 0;   /* last selection bound per op kind */
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
 #ifdef FD_POOL_STAMPS
   unsigned long ps[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
   unsigned long ps2[4] = { 0, 0, 0, 0 };
@@ -1412,6 +1435,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     ps2[0] += pta - pt0; ps2[1] += ptb - pta; ps2[2] += pt1 - ptb;
 #endif
   }
+  fd_clk_add( 0, clk_c0, clk_r0, lane );
 #ifdef FD_POOL_STAMPS
   ps[7] = __builtin_amdgcn_s_memtime() - pt_start;
   if( lane == 0 && gw < 65536u )

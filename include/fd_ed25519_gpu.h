@@ -335,6 +335,15 @@ int fd_ed25519_gpu_kernel_cnt( void );
 int fd_ed25519_gpu_dev_stats_begin( fd_ed25519_gpu_t * gpu );
 int fd_ed25519_gpu_dev_stats_end  ( fd_ed25519_gpu_t * gpu, float * kernel_ms_sum, unsigned long * launches );
 
+/* Shader clock the DSM kernels ran at on the engine's device: every wave
+   of fd_k_dsm_pool / fd_k_dsm_quad adds its main loop's shader cycles and
+   100 MHz real-time ticks to device-wide sums.  clear != 0 zeroes them;
+   otherwise out[6] = { pool waves, pool cycles, pool ticks, quad waves,
+   quad cycles, quad ticks } (GHz = 0.1 * cycles / ticks).  Call with the
+   device idle (it copies synchronously); sums are per device, shared by
+   every engine on it. */
+int fd_ed25519_gpu_dsm_clock( fd_ed25519_gpu_t * gpu, int clear, unsigned long long * out );
+
 /* Device the engine runs on; last HIP error string (diagnostics). */
 int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
 char const * fd_ed25519_gpu_last_error( void );

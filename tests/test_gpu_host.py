@@ -97,6 +97,32 @@ def test_pipelined_stats_attribute_setup_and_pool():
     e.close()
 
 
+def test_dsm_clock_counts_pool_and_quad_waves():
+    """fd_ed25519_gpu_dsm_clock: every pool / quad wave adds its loop's
+    shader cycles and real-time ticks; the ratio is a plausible gfx950 clock
+    (the bench reports it beside the roofline)"""
+    e = fa.Engine(0, 1 << 18, 1 << 29)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for n, pool_min in ((1 << 18, 0), (4096, 1 << 30)):
+        b = corpus.solana_txns(n, seed=34)
+        e.dsm_pool_min = pool_min
+        d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
+        d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+        d_out = torch.zeros(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        e.dsm_clock(clear=True)
+        e.verify_dev(n, d_blob.data_ptr(), len(b.blob), d_desc.data_ptr(), d_out.data_ptr(), st)
+        torch.cuda.synchronize()
+        c = e.dsm_clock()
+        assert (d_out.cpu().numpy() == 0).sum() >= n - 4
+        k, other = ("pool", "quad") if pool_min == 0 else ("quad", "pool")
+        assert c[k]["waves"] == (n // 128 if k == "pool" else n // 16), c
+        assert 1.0 < c[k]["ghz"] < 3.0, c
+        assert c[other]["waves"] == 0 and c[other]["ghz"] is None, c
+    e.close()
+
+
 @pytest.mark.parametrize("period_ns", [0, 150_000])
 def test_synth_producer_codes(ref, period_ns):
     base = corpus.adversarial_txns(20000, seed=33, invalid_frac=0.1)
