@@ -182,6 +182,10 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_set_dsm_quad_max.restype = ip
         L.fd_ed25519_gpu_dsm_quad_max.argtypes = [vp]
         L.fd_ed25519_gpu_dsm_quad_max.restype = ul
+        L.fd_ed25519_gpu_set_dsm_oct_max.argtypes = [vp, ul]
+        L.fd_ed25519_gpu_set_dsm_oct_max.restype = ip
+        L.fd_ed25519_gpu_dsm_oct_max.argtypes = [vp]
+        L.fd_ed25519_gpu_dsm_oct_max.restype = ul
         L.fd_ed25519_gpu_multi_new.argtypes = [vp, ip, ul, ul]
         L.fd_ed25519_gpu_multi_new.restype = vp
         L.fd_ed25519_gpu_multi_delete.argtypes = [vp]
@@ -319,9 +323,9 @@ class Engine:
     def dsm_clock(self, clear: bool = False):
         """Shader clock the DSM kernels ran at on this engine's device since
         the last clear (fd_ed25519_gpu_dsm_clock): None after clear=True,
-        else {"pool": {"waves", "ghz"}, "quad": {...}} (ghz None when no wave
+        else {"pool": {"waves", "ghz"}, "quad": {...}, "oct": {...}} (ghz None when no wave
         of that kernel ran).  Call with the device idle."""
-        out = np.zeros(6, np.uint64)
+        out = np.zeros(9, np.uint64)
         err = lib().fd_ed25519_gpu_dsm_clock(self._h, 1 if clear else 0, None if clear else _p(out))
         if err:
             raise EngineError(f"dsm_clock: {strerror(err)}: {last_error()}")
@@ -329,7 +333,7 @@ class Engine:
             return None
         def one(w, c, t):
             return {"waves": int(w), "ghz": (0.1 * float(c) / float(t)) if t else None}
-        return {"pool": one(*out[0:3]), "quad": one(*out[3:6])}
+        return {"pool": one(*out[0:3]), "quad": one(*out[3:6]), "oct": one(*out[6:9])}
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:
         """Queue a batch on the pinned ring; returns its ticket."""
@@ -380,7 +384,7 @@ class Engine:
         return k, st
 
     def debug_fe(self, op: int, f: np.ndarray, g: np.ndarray) -> np.ndarray:
-        """Diagnostics: the device field products (fd_k_debug_fe op 0-6) of
+        """Diagnostics: the device field products (fd_k_debug_fe op 0-6, op 7 the oct DSM's half product) of
         operand pairs f, g ([n,10] int32 limbs) -> [3,n,10] int32 limbs."""
         f = np.ascontiguousarray(f, dtype=np.int32).reshape(-1, 10)
         g = np.ascontiguousarray(g, dtype=np.int32).reshape(-1, 10)
@@ -441,6 +445,16 @@ class Engine:
     def dsm_quad_max(self, n: int) -> None:
         if lib().fd_ed25519_gpu_set_dsm_quad_max(self._h, n):
             raise EngineError("set_dsm_quad_max")
+
+    @property
+    def dsm_oct_max(self) -> int:
+        """batches of at most this many signatures (below dsm_pool_min) run the eight-lane DSM"""
+        return lib().fd_ed25519_gpu_dsm_oct_max(self._h)
+
+    @dsm_oct_max.setter
+    def dsm_oct_max(self, n: int) -> None:
+        if lib().fd_ed25519_gpu_set_dsm_oct_max(self._h, n):
+            raise EngineError("set_dsm_oct_max")
 
     @property
     def depth(self) -> int:

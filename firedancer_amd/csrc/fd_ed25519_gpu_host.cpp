@@ -141,6 +141,7 @@ struct fd_ed25519_gpu {
   int           mode;     /* FD_ED25519_GPU_MODE_* */
   unsigned long pool_min; /* batches >= this take the pooled DSM */
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
+  unsigned long oct_max;  /* and batches <= this the eight-lane DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
@@ -250,6 +251,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
+  g->oct_max  = FD_DSM_OCT_MAX_DEFAULT;
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );
   { char const * ga = getenv( "FD_ED25519_GPU_GROUP_ALWAYS" ); g->group_always = ga && atoi( ga ); }  /* experiments */
@@ -395,10 +397,10 @@ extern "C" int fd_ed25519_gpu_cu_groups( fd_ed25519_gpu_t const * g ) { return g
 /* the schedule knobs are set under the engine lock and read under it:
    submitters, the device-resident path and the feeder thread may run
    concurrently with a setter */
-struct fd_knobs { int mode; unsigned long pool_min, quad_max; };
+struct fd_knobs { int mode; unsigned long pool_min, quad_max, oct_max; };
 static fd_knobs fd_knobs_get( fd_ed25519_gpu_t const * g ) {
   std::lock_guard<std::mutex> guard( const_cast<fd_ed25519_gpu_t *>( g )->lock );
-  fd_knobs k = { g->mode, g->pool_min, g->quad_max };
+  fd_knobs k = { g->mode, g->pool_min, g->quad_max, g->oct_max };
   return k;
 }
 
@@ -499,6 +501,13 @@ extern "C" int fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * g, unsigned l
   return 0;
 }
 extern "C" unsigned long fd_ed25519_gpu_dsm_quad_max( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).quad_max : 0UL; }
+extern "C" int fd_ed25519_gpu_set_dsm_oct_max( fd_ed25519_gpu_t * g, unsigned long n ) {
+  if( !g ) return FD_ED25519_ERR_ARG;
+  std::lock_guard<std::mutex> guard( g->lock );
+  g->oct_max = n;
+  return 0;
+}
+extern "C" unsigned long fd_ed25519_gpu_dsm_oct_max( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).oct_max : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
 
@@ -586,11 +595,11 @@ static int fd_dev_launch( fd_ed25519_gpu_t * g, unsigned long n, void const * d_
     if( (e = hipEventRecord( g->dev_in[b], st )) != hipSuccess
      || (e = hipStreamWaitEvent( g->dev_sf, g->dev_in[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (inputs)", e );
   if( (e = hipStreamWaitEvent( g->dev_sf, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (front)", e );
-  if( (e = fd_ed25519_gpu_launch_front( n, (uint8_t const *)d_blob, blob_sz, d_desc, w, g->dev_sf, ev, mode, kn.pool_min, kn.quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch_front( n, (uint8_t const *)d_blob, blob_sz, d_desc, w, g->dev_sf, ev, mode, kn.pool_min, kn.quad_max, kn.oct_max )) != hipSuccess )
     return fd_gpu_fail( "fd_ed25519_gpu_launch_front", e );
   if( (e = hipEventRecord( g->dev_front[b], g->dev_sf )) != hipSuccess
    || (e = hipStreamWaitEvent( g->dev_sb, g->dev_front[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (back)", e );
-  if( (e = fd_ed25519_gpu_launch_back( n, (uint8_t const *)d_blob, d_desc, w, (int32_t *)d_out, g->dev_sb, ev, mode, kn.pool_min, kn.quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch_back( n, (uint8_t const *)d_blob, d_desc, w, (int32_t *)d_out, g->dev_sb, ev, mode, kn.pool_min, kn.quad_max, kn.oct_max )) != hipSuccess )
     return fd_gpu_fail( "fd_ed25519_gpu_launch_back", e );
   if( (e = hipEventRecord( g->dev_back[b], g->dev_sb )) != hipSuccess
    || (e = hipStreamWaitEvent( st, g->dev_back[b], 0 )) != hipSuccess ) return fd_gpu_fail( "dev order (caller)", e );
@@ -637,7 +646,7 @@ extern "C" int fd_ed25519_gpu_dev_stats_end( fd_ed25519_gpu_t * g, float * kerne
 }
 
 /* the DSM kernels' clock accumulators (fd_dsm_clk, kernels.hip): clear, or
-   read [pool waves, cycles, ticks, quad waves, cycles, ticks] */
+   read [waves, cycles, ticks] of the pool, quad and oct DSMs */
 extern "C" hipError_t fd_ed25519_gpu_dsm_clk_xfer( unsigned long long * host, int clear );
 extern "C" int fd_ed25519_gpu_dsm_clock( fd_ed25519_gpu_t * g, int clear, unsigned long long * out ) {
   if( !g || (!clear && !out) ) return FD_ED25519_ERR_ARG;
@@ -692,7 +701,7 @@ extern "C" int fd_ed25519_gpu_verify_dev_timed( fd_ed25519_gpu_t * g, unsigned l
   int mode = kn.mode;
   if( (e0 = fd_dev_serial_begin( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   if( (e0 = fd_ed25519_gpu_launch_timed( n, (uint8_t const *)d_blob, blob_sz, d_desc, &g->dev_work[0], (int32_t *)d_out, st, g->kev,
-                                         mode, kn.pool_min, kn.quad_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
+                                         mode, kn.pool_min, kn.quad_max, kn.oct_max )) != hipSuccess ) return fd_gpu_fail( "fd_ed25519_gpu_launch", e0 );
   if( (e0 = fd_dev_serial_end( g, st )) != hipSuccess ) return fd_gpu_fail( "dev order", e0 );
   int err;
   if( (err = fd_event_wait( g->kev[FD_ED25519_GPU_KERNEL_CNT], fd_timeout( g ) )) ) return err;
@@ -739,7 +748,7 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max )) != hipSuccess )
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max, g->oct_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
@@ -842,11 +851,12 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   return 1;
 }
 
-/* Diagnostics: the device field products (fd_k_debug_fe, ops 0-6) over n
+/* Diagnostics: the device field products (fd_k_debug_fe, ops 0-6; op 7
+   the oct DSM's half product, fd_k_debug_oct) over n
    operand pairs f, g ([n][10] int32 limbs); h receives [3][n][10] limbs.
    Synchronous; host buffers; n <= 2^20. */
 extern "C" int fd_ed25519_gpu_debug_fe( fd_ed25519_gpu_t * g, int op, unsigned long n, int const * f, int const * gg, int * h ) {
-  if( !g || op < 0 || op > 6 || n > (1UL<<20) || (n && (!f || !gg || !h)) ) return FD_ED25519_ERR_ARG;
+  if( !g || op < 0 || op > 7 || n > (1UL<<20) || (n && (!f || !gg || !h)) ) return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );

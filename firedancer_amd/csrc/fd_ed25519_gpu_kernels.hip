@@ -53,12 +53,12 @@ __device__ static int32_t fd_gpu_bi_tab[8*FD_TAB_ENTRY];
    cycles (s_memtime) and 100 MHz real-time ticks (s_memrealtime), summed
    with one vector atomic each from lane 0 (a few per 1,000 signatures):
    [0] waves, [1] cycles, [2] ticks of fd_k_dsm_pool; [3..5] the same for
-   fd_k_dsm_quad.  cycles / ticks x 0.1 GHz is the clock the kernel ran at,
-   which separates a box's DVFS state from a code regression in the
-   bench's roofline (fd_ed25519_gpu_dsm_clock). */
-__device__ unsigned long long fd_dsm_clk[6];
+   fd_k_dsm_quad, [6..8] for fd_k_dsm_oct.  cycles / ticks x 0.1 GHz is the
+   clock the kernel ran at, which separates a box's DVFS state from a code
+   regression in the bench's roofline (fd_ed25519_gpu_dsm_clock). */
+__device__ unsigned long long fd_dsm_clk[9];
 extern "C" hipError_t fd_ed25519_gpu_dsm_clk_xfer( unsigned long long * host, int clear ) {
-  if( clear ) { static unsigned long long const z[6] = { 0, 0, 0, 0, 0, 0 }; return hipMemcpyToSymbol( HIP_SYMBOL(fd_dsm_clk), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  if( clear ) { static unsigned long long const z[9] = { 0, 0, 0, 0, 0, 0, 0, 0, 0 }; return hipMemcpyToSymbol( HIP_SYMBOL(fd_dsm_clk), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
   return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_dsm_clk), sizeof(fd_dsm_clk), 0, hipMemcpyDeviceToHost );
 }
 FD_DEV void fd_clk_add( int k, unsigned long long c0, unsigned long long r0, uint32_t lane ) {
@@ -214,8 +214,10 @@ FD_DEV int fd_wave_max( int x ) {
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only: [0] prep round wave, [1] decomp, [2] prep
    schedule wave, [3] prep round wave up to its digest (the rest of [0] is
-   sc_reduce, the recoder and the op row) -- per-wave times in 2 us bins */
-__device__ unsigned long long fd_front_hist[4][256];
+   sc_reduce, the recoder and the op row) -- per-wave times in 2 us bins;
+   [4] the round wave's sc_reduce, [5] its op-row zeroing + recoder, in
+   0.2 us bins */
+__device__ unsigned long long fd_front_hist[6][256];
 #endif
 static __device__ __forceinline__ void
 fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
@@ -281,14 +283,28 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
 #pragma unroll
   for( int j=0; j<8; j++ ) dig[j] = fd_bswap64( dig[j] );
   uint64_t k[4];
+#ifdef FD_FRONT_STAMPS
+  unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
   fd_sc_reduce( k, dig );
   uint32_t kw[8];
 #pragma unroll
   for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
+#ifdef FD_FRONT_STAMPS
+  unsigned long long ts2 = __builtin_amdgcn_s_memrealtime();
+#endif
   int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
 #pragma unroll
   for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
   op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
+#ifdef FD_FRONT_STAMPS
+  {
+    unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
+    unsigned b4 = (unsigned)((ts2 - ts1) / 20ULL), b5 = (unsigned)((ts3 - ts2) / 20ULL);
+    atomicAdd( &fd_front_hist[4][b4 > 255u ? 255u : b4], 1ULL );
+    atomicAdd( &fd_front_hist[5][b5 > 255u ? 255u : b5], 1ULL );
+  }
+#endif
 }
 
 extern "C" __global__ void __launch_bounds__(256, 4)
@@ -482,7 +498,7 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
    bins) for prep and decomp waves, accumulated over every launch with
    vector atomics */
 extern "C" hipError_t fd_ed25519_gpu_front_hist( void * host, int clear ) {
-  if( clear ) { static unsigned long long z[4][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
+  if( clear ) { static unsigned long long z[6][256]; return hipMemcpyToSymbol( HIP_SYMBOL(fd_front_hist), z, sizeof(z), 0, hipMemcpyHostToDevice ); }
   return hipMemcpyFromSymbol( host, HIP_SYMBOL(fd_front_hist), sizeof(fd_front_hist), 0, hipMemcpyDeviceToHost );
 }
 #endif
@@ -1064,6 +1080,368 @@ fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 }
 
 /* ------------------------------------------------------------------ */
+/* Kernel 3 for single signatures and tiny batches (n <= oct_max, default
+   64: the per-signature drop-in and group commits): EIGHT lanes per
+   signature.  The quad's lane q is split in two halves: in the even rows
+   of the wave (h = 0) a lane holds limbs 0-4 of each field element of AVX
+   lane q, the lane 16 above it (h = 1) limbs 5-9.  What the quad does limb
+   by limb -- the DPP quad permutations, the op's operand selects and
+   output mixes -- then costs each lane half as much.  A product exchanges
+   the halves' operand limbs (v_permlane16_swap_b32 swaps rows 2k and
+   2k+1), each lane forms five of the ten column sums (50 MACs), and the
+   reference's 12-step carry chain runs split over the halves with two
+   cross-half carries.  Same products, pre-scaled operands, column sums
+   and carry sequence as the quad, so the limbs are identical
+   (tests/test_fe_gpu.py op 7, tests/test_gpu_parity.py::test_oct_*).
+
+   Column sums of a half: slot j is column K = 5h + j.  h = 1 lanes see g
+   rotated by five limbs (G = [own limbs, partner limbs]), which makes the
+   g index of term (j, J') the same J' in both halves with f index
+   I = (j - J') mod 10, f in natural order.  The AVX MUL convention
+   (fd_mul_cols: 2f when f index and g index are both odd, 19g when the
+   term wraps, K - I < 0) becomes, per lane: 2f when I is odd and J' odd
+   XOR h, i.e. f << (1-h) for odd J' and f << h for even J'; 19G for
+   j < J' < 5 in both halves and, for J' >= 5, 19G in h = 0 and G in
+   h = 1. */
+#define FD_OSIGS      8       /* signatures per 64-lane wave */
+#define FD_OTAB_LANE  16      /* an entry lane: limbs 0-4, 3 pad, limbs 5-9, 3 pad (each half 32-byte aligned) */
+#define FD_OTAB_ENTRY (4*FD_OTAB_LANE)
+typedef struct { int32_t v[5]; } fh;   /* a lane's half of a field element */
+
+/* x of this lane's row-pair partners: a = the even-row lane's, b = the
+   odd-row lane's, in every lane (v_permlane16_swap_b32 swaps the odd rows
+   of its first operand with the even rows of its second) */
+FD_QDEV void fd_o_both( int32_t x, int32_t & a, int32_t & b ) {
+  auto r = __builtin_amdgcn_permlane16_swap( (uint32_t)x, (uint32_t)x, false, false );
+  a = (int32_t)r[0]; b = (int32_t)r[1];
+}
+FD_QDEV void fd_o_both64( int64_t x, int64_t & a, int64_t & b ) {
+  int32_t al, bl, ah, bh;
+  fd_o_both( (int32_t)(uint32_t)x, al, bl );
+  fd_o_both( (int32_t)(uint32_t)((uint64_t)x >> 32), ah, bh );
+  a = (int64_t)(((uint64_t)(uint32_t)ah << 32) | (uint32_t)al);
+  b = (int64_t)(((uint64_t)(uint32_t)bh << 32) | (uint32_t)bl);
+}
+/* m ? a : b for 64-bit values, a lane mask m in {0, ~0} */
+FD_QDEV int64_t fd_sel64( uint32_t m, int64_t a, int64_t b ) {
+  uint32_t lo = fd_sel( m, (uint32_t)a, (uint32_t)b );
+  uint32_t hi = fd_sel( m, (uint32_t)((uint64_t)a >> 32), (uint32_t)((uint64_t)b >> 32) );
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+/* per-lane constants of a half (value barriers: LLVM would otherwise
+   rebuild them from h at every use) */
+struct fd_octc {
+  uint32_t hm;          /* ~0 on h = 1 lanes */
+  uint32_t sA, sB;      /* 2f shifts for odd / even J': 1-h, h */
+  uint32_t m19;         /* the J' >= 5 wrap factor: 19 (h = 0), 1 (h = 1) */
+  uint32_t wE, wO;      /* carry widths of even / odd slots (column parity is slot parity XOR h) */
+  uint32_t mE, mO;      /* their residual masks */
+  uint32_t bE, bO;      /* their column biases 2^(w-1) */
+};
+FD_QDEV fd_octc fd_octc_make( uint32_t h ) {
+  fd_octc c;
+  c.hm  = (uint32_t)fd_opaque( h ? -1 : 0 );
+  c.sA  = (uint32_t)fd_opaque( (int32_t)(1u - h) );
+  c.sB  = (uint32_t)fd_opaque( (int32_t)h );
+  c.m19 = (uint32_t)fd_opaque( h ? 1 : 19 );
+  c.wE  = (uint32_t)fd_opaque( h ? 25 : 26 );
+  c.wO  = (uint32_t)fd_opaque( h ? 26 : 25 );
+  c.mE  = (uint32_t)fd_opaque( (int32_t)((1u << (h ? 25 : 26)) - 1u) );
+  c.mO  = (uint32_t)fd_opaque( (int32_t)((1u << (h ? 26 : 25)) - 1u) );
+  c.bE  = (uint32_t)fd_opaque( (int32_t)(h ? (1u<<24) : (1u<<25)) );
+  c.bO  = (uint32_t)fd_opaque( (int32_t)(h ? (1u<<25) : (1u<<24)) );
+  return c;
+}
+
+/* operands of one product, both halves' limbs in every lane */
+struct fd_oops {
+  int32_t F[10];     /* f, natural order */
+  int32_t FA[10];    /* odd I: f << (1-h) (terms with odd J') */
+  int32_t FB[10];    /* odd I: f << h     (terms with even J') */
+  int32_t G[10];     /* g rotated for h = 1: [own limbs, partner limbs] */
+  int32_t G19[10];   /* J' 1-4: 19 G; J' 5-9: 19 G (h = 0) or G (h = 1) */
+};
+template<int J, int JP> FD_QDEV int64_t fd_o_term( fd_oops const & o, int64_t acc ) {
+  constexpr int I = (J - JP + 10) % 10;
+  int32_t const fo = (I & 1) ? ((JP & 1) ? o.FA[I] : o.FB[I]) : o.F[I];
+  int32_t const go = (JP <= J) ? o.G[JP] : o.G19[JP];
+  return fd_mad( fo, go, acc );
+}
+template<int JP> FD_QDEV void fd_o_terms( fd_oops const & o, int64_t (&S)[5] ) {
+  S[0] = fd_o_term<0,JP>( o, S[0] ); S[1] = fd_o_term<1,JP>( o, S[1] ); S[2] = fd_o_term<2,JP>( o, S[2] );
+  S[3] = fd_o_term<3,JP>( o, S[3] ); S[4] = fd_o_term<4,JP>( o, S[4] );
+}
+
+/* carry of slot j into slot j+1 (biased sums: the carry is a bare shift,
+   the residual the low w bits, fd_fe_carry) */
+FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
+  int64_t cy = s >> w;
+  s = (int64_t)(uint64_t)((uint32_t)s & m);
+  nx += cy;
+}
+
+/* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9) */
+FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c ) {
+  fd_oops o;
+#pragma unroll
+  for( int j=0; j<5; j++ ) {
+    fd_o_both( f.v[j], o.F[j], o.F[5+j] );
+    int32_t a, b; fd_o_both( g.v[j], a, b );
+    o.G[j] = g.v[j]; o.G[5+j] = (int32_t)fd_sel( c.hm, (uint32_t)a, (uint32_t)b );
+  }
+#pragma unroll
+  for( int i=1; i<10; i+=2 ) {
+    o.FA[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sA) );
+    o.FB[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sB) );
+  }
+  o.G19[0] = 0;
+#pragma unroll
+  for( int j=1; j<5; j++ )  o.G19[j] = fd_opaque( (int32_t)(19u   * (uint32_t)o.G[j]) );
+#pragma unroll
+  for( int j=5; j<10; j++ ) o.G19[j] = fd_opaque( (int32_t)(c.m19 * (uint32_t)o.G[j]) );
+
+  int64_t S[5];
+  S[0] = fd_opaque64( (int64_t)c.bE ); S[1] = fd_opaque64( (int64_t)c.bO ); S[2] = fd_opaque64( (int64_t)c.bE );
+  S[3] = fd_opaque64( (int64_t)c.bO ); S[4] = fd_opaque64( (int64_t)c.bE );
+  fd_o_terms<0>( o, S ); fd_o_terms<1>( o, S ); fd_o_terms<2>( o, S ); fd_o_terms<3>( o, S ); fd_o_terms<4>( o, S );
+  fd_o_terms<5>( o, S ); fd_o_terms<6>( o, S ); fd_o_terms<7>( o, S ); fd_o_terms<8>( o, S ); fd_o_terms<9>( o, S );
+
+  /* the reference's chain 0,4,1,5,2,6,3,7,4,8,9,0 (fd_fe_carry) as
+     A: c4 (h = 0's slot 4) into limb 5; B-E: 0->1 | 5->6 ... 3->4 | 8->9 in
+     both halves at once; F: c4' into limb 5 and 19 c9 into limb 0 across;
+     G: c0' (h = 0) */
+  uint64_t const hm64 = ((uint64_t)c.hm << 32) | c.hm;
+  {
+    int64_t cy = S[4] >> c.wE;
+    S[4] = fd_sel64( c.hm, S[4], (int64_t)(uint64_t)((uint32_t)S[4] & c.mE) );
+    int64_t a, b; fd_o_both64( cy, a, b );
+    S[0] += (int64_t)((uint64_t)a & hm64);
+  }
+  fd_o_carry( S[0], S[1], c.wE, c.mE );
+  fd_o_carry( S[1], S[2], c.wO, c.mO );
+  fd_o_carry( S[2], S[3], c.wE, c.mE );
+  fd_o_carry( S[3], S[4], c.wO, c.mO );
+  {
+    int64_t cy = S[4] >> c.wE;
+    S[4] = (int64_t)(uint64_t)((uint32_t)S[4] & c.mE);
+    int64_t a, b; fd_o_both64( cy, a, b );
+    S[0] += fd_sel64( c.hm, a, b * 19 );
+  }
+  {
+    int64_t cy = (int64_t)((uint64_t)(S[0] >> c.wE) & ~hm64);
+    S[0] = fd_sel64( c.hm, S[0], (int64_t)(uint64_t)((uint32_t)S[0] & c.mE) );
+    S[1] += cy;
+  }
+  out.v[0] = fd_opaque( (int32_t)((uint32_t)S[0] - c.bE) );
+  out.v[1] = fd_opaque( (int32_t)((uint32_t)S[1] - c.bO) );
+  out.v[2] = fd_opaque( (int32_t)((uint32_t)S[2] - c.bE) );
+  out.v[3] = fd_opaque( (int32_t)((uint32_t)S[3] - c.bO) );
+  out.v[4] = fd_opaque( (int32_t)((uint32_t)S[4] - c.bE) );
+}
+
+template<int CTRL> FD_QDEV void fd_fh_qperm( fh & o, fh const & x ) {
+#pragma unroll
+  for( int k=0; k<5; k++ ) o.v[k] = fd_qperm<CTRL>( x.v[k] );
+}
+/* this lane's half of v (limbs 5h..5h+4) */
+FD_QDEV fh fd_fh_own( fe const & v, uint32_t hm ) {
+  fh x;
+#pragma unroll
+  for( int j=0; j<5; j++ ) x.v[j] = (int32_t)fd_sel( hm, (uint32_t)v.v[5+j], (uint32_t)v.v[j] );
+  return x;
+}
+/* the whole field element from the halves of this lane's row pair */
+FD_QDEV void fd_fh_full( fe & v, fh const & x ) {
+#pragma unroll
+  for( int j=0; j<5; j++ ) fd_o_both( x.v[j], v.v[j], v.v[5+j] );
+}
+
+struct fd_oct_lds {
+  int32_t tab[FD_OSIGS+1][8*FD_OTAB_ENTRY];   /* Ai per signature, [FD_OSIGS] = Bi */
+  uint8_t ops[FD_OSIGS][FD_QOPS_ROW];
+};
+
+extern "C" __global__ void __launch_bounds__(64)
+fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+              int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
+              int32_t * __restrict__ out, int strict ) {
+  __shared__ __attribute__((aligned(16))) fd_oct_lds L;
+  uint32_t lane = threadIdx.x;
+  uint32_t q  = lane & 3u, h = (lane >> 4) & 1u;
+  uint32_t ls = ((lane >> 5) << 2) | ((lane >> 2) & 3u);   /* signature slot of the wave */
+  uint64_t sig0 = (uint64_t)blockIdx.x * FD_OSIGS;
+  uint64_t i    = sig0 + ls;
+  int live = i < n;
+  uint64_t ii = live ? i : 0;
+  uint64_t m = 2*n;
+  int st = status[ii];
+  int pa = pstat[ii], pr = pstat[n+ii];
+  int code;
+  /* error precedence (fd_ed25519_user.c:372-403), as the quad */
+  if( st != FD_ST_PENDING )                        code = st;
+  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
+  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
+  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
+  else                                             code = FD_ST_PENDING;
+  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
+
+  uint32_t const comp = q==0u ? 20u : q==1u ? 10u : q==2u ? 0u : 30u;
+  fe r, rr;
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    int32_t x = pts[(uint64_t)(comp+k)*m + ii];
+    r.v[k]  = q >= 2u ? (int32_t)(0u - (uint32_t)x) : x;
+    rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
+  }
+
+  int t0 = fd_wave_min( start );
+  {
+    int const c0 = t0 >> 4;
+    for( int c=(int)lane; c<FD_OSIGS*(FD_OPS_MAX/16); c+=64 ) {
+      int sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
+      if( ch < c0 ) continue;
+      uint64_t gs = sig0 + (uint64_t)sg;
+      int4 v = gs < n ? *(int4 const *)(ops + gs*FD_OPS_MAX + (uint64_t)ch*16u) : make_int4( 0, 0, 0, 0 );
+      *(int4 *)&L.ops[sg][ch*16] = v;
+    }
+    /* Bi into the half-aligned entry layout */
+    for( int k=lane; k<8*4*10; k+=64 ) {
+      int e = k / 40, l = (k / 10) % 4, limb = k % 10;
+      L.tab[FD_OSIGS][e*FD_OTAB_ENTRY + l*FD_OTAB_LANE + (limb < 5 ? limb : limb + 3)] = fd_gpu_bi_tab[e*FD_TAB_ENTRY + l*FD_TAB_LANE + limb];
+    }
+  }
+
+  uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
+  uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
+  fd_octc const oc = fd_octc_make( h );
+
+  /* Ai = {A,3A,...,15A}: the quad's prologue on whole field elements
+     (both halves compute it), each lane storing its half */
+  fe one; fd_fe_set( one, 1 );
+  fe d111 = q==3u ? FD_GPU_D2 : one;
+  int32_t * tab_s = L.tab[ls] + q*FD_OTAB_LANE + 8u*h;
+  fe vu, vt, f, g;
+  FD_QMUL( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
+  {
+    fh x = fd_fh_own( vu, oc.hm );
+    ((int4 *)tab_s)[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); ((int4 *)tab_s)[1] = make_int4( x.v[4], 0, 0, 0 );
+  }
+  {
+    fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      f.v[k] = (int32_t)((uint32_t)a.v[k] + ((uint32_t)b.v[k] & mq0));
+      g.v[k] = (int32_t)((uint32_t)f.v[k] << (q==3u ? 1 : 0));
+    }
+    FD_QMUL( vt, f, g );
+    fd_q_dblmix( vt, m03, s02 );
+  }
+  fd_fe_qperm<FD_QP(3,2,3,1)>( f, vt ); fd_fe_qperm<FD_QP(2,1,0,0)>( g, vt );
+  FD_QMUL( r, f, g ); fd_q_subadd12( r, m12, mq1 );
+  for( int e=0; e<7; e++ ) {
+    FD_QMUL( vt, r, vu );
+    fd_q_submix( vt, q >> 1, (q & 1u) ? 0u : ~0u );
+    fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
+    FD_QMUL( vt, f, g );
+    FD_QMUL( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
+    fh x = fd_fh_own( vu, oc.hm );
+    int4 * p = (int4 *)(tab_s + (e+1)*FD_OTAB_ENTRY);
+    p[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); p[1] = make_int4( x.v[4], 0, 0, 0 );
+  }
+  __syncthreads();
+
+  /* main loop: the quad's step on half field elements */
+  fh s;
+#pragma unroll
+  for( int k=0; k<5; k++ ) s.v[k] = 0;
+  s.v[0] = (int32_t)((q && !h) ? 1 : 0);
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long os_c0 = __builtin_amdgcn_s_memtime(), os_r0 = __builtin_amdgcn_s_memrealtime();
+  for( int t=t0; t<FD_OPS_MAX; t++ ) {
+    int op = (int)L.ops[ls][t];
+    uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
+    uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
+    uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
+    int32_t E[5];
+    {
+      int32_t const * ent = ((op & 0x40) ? L.tab[FD_OSIGS] : L.tab[ls]) + (op & 7)*FD_OTAB_ENTRY + idx*FD_OTAB_LANE + 8u*h;
+      int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1];
+      E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x;
+    }
+
+    fh fo, go, C;
+    fd_fh_qperm<FD_QP(2,1,0,0)>( fo, s ); fd_fh_qperm<FD_QP(3,2,3,1)>( go, s );
+    fd_o_mul( C, fo, go, oc );
+
+    fh u, w;
+    fd_fh_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fh_qperm<FD_QP(2,2,2,2)>( w, C );
+    uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
+    uint32_t gs = (q==1u && !add) ? 1u : 0u;
+    uint32_t const s2b = (uint32_t)fd_opaque( (int32_t)(mq2 & 1u) );
+#pragma unroll
+    for( int k=0; k<5; k++ ) {
+      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_andxor( (uint32_t)w.v[k], mW, mq2 ) + s2b );
+      fo.v[k] = (int32_t)fk;
+      go.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
+    }
+    fh hq; fd_o_mul( hq, fo, go, oc );
+
+    uint32_t pos = add & ~neg;
+    uint32_t mP = mq0 | (mq1 & add);
+    uint32_t mQ = mq3 | (mq2 & add), qs = add ? 1u : 0u;
+    uint32_t mR = mq0 | mq1 | ~add, sR = mq0 | (mq3 & ~add);
+    uint32_t mS = ~((mq0 | mq1) & add), sS = (mq0 & ~add) | (mq2 & ~pos) | (mq3 & pos);
+    uint32_t cadd = (sR & 1u) + (sS & 1u);
+    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
+    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
+#pragma unroll
+    for( int k=0; k<5; k++ ) {
+      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( hq.v[k] ) & mPv) );
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( hq.v[k] ) & mQv) );
+      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( hq.v[k] ) & mRv) );
+      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( hq.v[k] ) & mSv) );
+      s.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + cadd);
+    }
+  }
+  fd_clk_add( 6, os_c0, os_r0, lane );
+
+  /* the whole final state, then the quad's final p1p1 -> p2 and the limb
+     compare (Q2) */
+  fd_fh_full( vt, s );
+  fe P2;
+  fd_fe_qperm<FD_QP(0,1,2,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
+  FD_QMUL( P2, f, g );
+  fd_fe_qperm<FD_QP(2,2,2,2)>( f, P2 );
+  fe cz; FD_QMUL( cz, f, rr );
+  int eq = 1;
+#pragma unroll
+  for( int k=0; k<8; k++ ) eq &= (cz.v[k] == P2.v[k]);
+  if( strict ) eq = fd_fe_value_eq( cz, P2 );
+  int eq1 = fd_qperm<FD_QP(1,1,1,1)>( eq );
+  if( code == FD_ST_PENDING ) code = (eq & eq1) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if( live && q == 0u && h == 0u ) out[i] = code;
+}
+
+/* diagnostics: fd_o_mul over n operand pairs ([n][10] limbs; h [n][10]),
+   lanes laid out as in fd_k_dsm_oct (pair = lane with its h bit removed) */
+extern "C" __global__ void __launch_bounds__(64)
+fd_k_debug_oct( uint64_t n, int32_t const * __restrict__ f, int32_t const * __restrict__ g, int32_t * __restrict__ hout ) {
+  uint32_t lane = threadIdx.x, h = (lane >> 4) & 1u;
+  uint64_t p = (uint64_t)blockIdx.x * 32u + ((lane >> 5) << 4) + (lane & 15u);
+  uint64_t pp = p < n ? p : n - 1;     /* every lane takes part in the exchanges */
+  fd_octc const oc = fd_octc_make( h );
+  fh a, b, r;
+#pragma unroll
+  for( int j=0; j<5; j++ ) { a.v[j] = f[pp*10 + 5u*h + j]; b.v[j] = g[pp*10 + 5u*h + j]; }
+  fd_o_mul( r, a, b, oc );
+  if( p < n ) {
+#pragma unroll
+    for( int j=0; j<5; j++ ) hout[p*10 + 5u*h + j] = r.v[j];
+  }
+}
+
+/* ------------------------------------------------------------------ */
 /* Kernel 3 as a signature pool (fd_k_dsm_setup -> fd_k_dsm_pool ->
    fd_k_dsm_final).  The uniform step above pays for both op kinds on
    every lane.  Here each wave owns a pool of FD_POOL signatures whose p1p1
@@ -1553,7 +1931,7 @@ extern "C" hipError_t fd_ed25519_gpu_upload_tables( void ) {
    schedule, the Ai tables (fd_k_dsm_setup).  Timing events ev[0..3]. */
 extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                                    fd_ed25519_gpu_work_t const * w, hipStream_t stream,
-                                                   hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
+                                                   hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max ) {
   if( !n ) return hipSuccess;
   mode &= 0xff;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
@@ -1561,7 +1939,8 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   unsigned nb  = (unsigned)((n + 255) / 256);
   unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
   if( ev ) hipEventRecord( ev[0], stream );
-  int quad = n < pool_min && !portable && n <= quad_max;
+  /* the quad and oct DSMs share the latency front end (signature-major op rows) */
+  int quad = n < pool_min && !portable && (n <= quad_max || n <= oct_max);
   /* step-major op streams are zero-filled first; the quad schedule's
      signature-major rows are zeroed by their own prep lanes (only rows of
      signatures still pending after the S check are ever read) */
@@ -1595,12 +1974,13 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
    Timing events ev[FD_EV_BACK], ev[4], ev[5]. */
 extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                  hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
+                                                  hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max ) {
   if( !n ) return hipSuccess;
   mode &= 0xff;
   int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
   int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
   unsigned nb  = (unsigned)((n + 255) / 256);
+  int oct  = n < pool_min && !portable && n <= oct_max;
   int quad = n < pool_min && !portable && n <= quad_max;
   if( n >= pool_min ) {
     uint32_t nw = (uint32_t)((n + FD_POOL - 1) / FD_POOL);  /* one full pool per wave */
@@ -1612,6 +1992,11 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
                         w->tab, w->fin, portable, nw );
     if( ev ) hipEventRecord( ev[4], stream );
     hipLaunchKernelGGL( fd_k_dsm_final, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->fin, out, blob, desc, portable, strict );
+  } else if( oct ) {
+    if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
+    hipLaunchKernelGGL( fd_k_dsm_oct, dim3((unsigned)((n + FD_OSIGS - 1) / FD_OSIGS)), dim3(64), 0, stream,
+                        n, w->status, w->pstat, w->pts, w->ops, w->op_start, out, strict );
+    if( ev ) hipEventRecord( ev[4], stream );
   } else if( quad ) {
     if( ev ) hipEventRecord( ev[FD_EV_BACK], stream );
     hipLaunchKernelGGL( fd_k_dsm_quad, dim3((unsigned)((n + FD_QSIGS - 1) / FD_QSIGS)), dim3(64), 0, stream,
@@ -1630,10 +2015,10 @@ extern "C" hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * bl
 /* both parts in order on one stream */
 extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                                     fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                                    hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max ) {
-  hipError_t e = fd_ed25519_gpu_launch_front( n, blob, blob_sz, desc, w, stream, ev, mode, pool_min, quad_max );
+                                                    hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max ) {
+  hipError_t e = fd_ed25519_gpu_launch_front( n, blob, blob_sz, desc, w, stream, ev, mode, pool_min, quad_max, oct_max );
   if( e != hipSuccess ) return e;
-  return fd_ed25519_gpu_launch_back( n, blob, desc, w, out, stream, ev, mode, pool_min, quad_max );
+  return fd_ed25519_gpu_launch_back( n, blob, desc, w, out, stream, ev, mode, pool_min, quad_max, oct_max );
 }
 
 /* diagnostics: fd_k_prep alone, writing each pending signature's k as
@@ -1661,7 +2046,8 @@ extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * 
      3 fd_fe_mul_ilp        h0 = f g            (independent column chains)
      4 fd_fe_mul2           h0 = f g, h1 = g f  (uniform DSM, pool additions)
      5 fd_fe_chain3         h0 = f g, h1 = g f, h2 = f f (pool p1p1 -> p2)
-     6 fd_fe_sqn2           h0 = f^2, h1 = 2 g^2 (pool doubling) */
+     6 fd_fe_sqn2           h0 = f^2, h1 = 2 g^2 (pool doubling)
+     7 fd_o_mul             h0 = f g            (oct DSM: two half lanes per product, fd_k_debug_oct) */
 extern "C" __global__ void __launch_bounds__(256)
 fd_k_debug_fe( int op, uint64_t n, int32_t const * __restrict__ f, int32_t const * __restrict__ g, int32_t * __restrict__ h ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1693,12 +2079,18 @@ fd_k_debug_fe( int op, uint64_t n, int32_t const * __restrict__ f, int32_t const
 extern "C" hipError_t fd_ed25519_gpu_launch_debug_fe( int op, uint64_t n, int32_t const * f, int32_t const * g, int32_t * h,
                                                      hipStream_t stream ) {
   if( !n ) return hipSuccess;
+  if( op == 7 ) {   /* the oct DSM's half product (fd_o_mul) */
+    hipError_t e = hipMemsetAsync( h + 10*n, 0, 2*n*10*sizeof(int32_t), stream );
+    if( e != hipSuccess ) return e;
+    hipLaunchKernelGGL( fd_k_debug_oct, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, stream, n, f, g, h );
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL( fd_k_debug_fe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, n, f, g, h );
   return hipGetLastError();
 }
 
 extern "C" hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                               fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
-                                              uint64_t pool_min, uint64_t quad_max ) {
-  return fd_ed25519_gpu_launch_timed( n, blob, blob_sz, desc, w, out, stream, NULL, mode, pool_min, quad_max );
+                                              uint64_t pool_min, uint64_t quad_max, uint64_t oct_max ) {
+  return fd_ed25519_gpu_launch_timed( n, blob, blob_sz, desc, w, out, stream, NULL, mode, pool_min, quad_max, oct_max );
 }

@@ -55,13 +55,13 @@ extern "C" {
 hipError_t fd_ed25519_gpu_upload_tables( void );
 hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                         fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max );
 hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                         fd_ed25519_gpu_work_t const * w, hipStream_t stream,
-                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+                                        hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max );
 hipError_t fd_ed25519_gpu_launch_back( uint64_t n, uint8_t const * blob, fd_ed25519_gpu_desc_t const * desc,
                                        fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
-                                       hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max );
+                                       hipEvent_t const * ev, int mode, uint64_t pool_min, uint64_t quad_max, uint64_t oct_max );
 hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                          fd_ed25519_gpu_work_t const * w, uint64_t * kout, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch_debug_fe( int op, uint64_t n, int32_t const * f, int32_t const * g, int32_t * h,
@@ -70,7 +70,7 @@ hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed
                                          void * out, int is384, hipStream_t stream );
 hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
-                                  uint64_t pool_min, uint64_t quad_max );
+                                  uint64_t pool_min, uint64_t quad_max, uint64_t oct_max );
 /* descriptor bounds: R||S, the key and the message inside blob[0, blob_sz)
    (64-bit sums, so no offset wraps) */
 static inline __host__ __device__ int fd_desc_in( fd_ed25519_gpu_desc_t const & d, uint64_t blob_sz ) {
@@ -81,6 +81,8 @@ static inline __host__ __device__ int fd_desc_in( fd_ed25519_gpu_desc_t const & 
 #define FD_DSM_POOL_MIN_DEFAULT (262144UL)
 /* smaller batches of at most this many signatures take the quad-lane DSM */
 #define FD_DSM_QUAD_MAX_DEFAULT (32768UL)
+/* batches of at most this many take the eight-lane DSM (fd_k_dsm_oct) */
+#define FD_DSM_OCT_MAX_DEFAULT (64UL)
 #ifdef __cplusplus
 }
 #endif

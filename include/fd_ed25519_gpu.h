@@ -291,6 +291,16 @@ unsigned long fd_ed25519_gpu_dsm_pool_min    ( fd_ed25519_gpu_t const * gpu );
 int           fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * gpu, unsigned long quad_max );
 unsigned long fd_ed25519_gpu_dsm_quad_max    ( fd_ed25519_gpu_t const * gpu );
 
+/* Batches below pool_min of at most oct_max signatures (default 64; AVX
+   and strict modes) run the DSM with eight lanes per signature: the quad's
+   lane q split into two halves of five limbs each, so every lane issues
+   half the quad's permutations, selects and mixes and half its multiplies
+   per step.  The per-signature drop-in and group commits land here.  It
+   takes precedence over quad_max.  Results are identical to the other
+   schedules.  0 = never. */
+int           fd_ed25519_gpu_set_dsm_oct_max( fd_ed25519_gpu_t * gpu, unsigned long oct_max );
+unsigned long fd_ed25519_gpu_dsm_oct_max    ( fd_ed25519_gpu_t const * gpu );
+
 /* Zero-copy staging: lend the pinned blob (max_blob + 64 bytes) and
    descriptor (max_sigs) buffers of a free ring slot.  The caller builds
    the batch in place and passes the same pointers to
@@ -336,12 +346,12 @@ int fd_ed25519_gpu_dev_stats_begin( fd_ed25519_gpu_t * gpu );
 int fd_ed25519_gpu_dev_stats_end  ( fd_ed25519_gpu_t * gpu, float * kernel_ms_sum, unsigned long * launches );
 
 /* Shader clock the DSM kernels ran at on the engine's device: every wave
-   of fd_k_dsm_pool / fd_k_dsm_quad adds its main loop's shader cycles and
-   100 MHz real-time ticks to device-wide sums.  clear != 0 zeroes them;
-   otherwise out[6] = { pool waves, pool cycles, pool ticks, quad waves,
-   quad cycles, quad ticks } (GHz = 0.1 * cycles / ticks).  Call with the
-   device idle (it copies synchronously); sums are per device, shared by
-   every engine on it. */
+   of fd_k_dsm_pool / fd_k_dsm_quad / fd_k_dsm_oct adds its main loop's
+   shader cycles and 100 MHz real-time ticks to device-wide sums.  clear !=
+   0 zeroes them; otherwise out[9] = { waves, cycles, ticks } of the pool,
+   the quad and the oct DSM in that order (GHz = 0.1 * cycles / ticks).
+   Call with the device idle (it copies synchronously); sums are per
+   device, shared by every engine on it. */
 int fd_ed25519_gpu_dsm_clock( fd_ed25519_gpu_t * gpu, int clear, unsigned long long * out );
 
 /* Device the engine runs on; last HIP error string (diagnostics). */

@@ -46,7 +46,7 @@ def test_device_field_products_vs_reference(engine, ref, bits):
     fg, gf, ff = ref_mul(ref, F, G), ref_mul(ref, G, F), ref_mul(ref, F, F)
     f2, g2x2 = ref_sqn(ref, F, 1), ref_sqn(ref, G, 2)
     f2x2 = ref_sqn(ref, F, 2)
-    H = {op: engine.debug_fe(op, F, G) for op in range(7)}
+    H = {op: engine.debug_fe(op, F, G) for op in range(8)}
     assert (H[0][0] == fg).all(), "fd_fe_mul"
     assert (H[1][0] == f2).all(), "fd_fe_sqn n=1"
     assert (H[2][0] == f2x2).all(), "fd_fe_sqn n=2"
@@ -54,10 +54,12 @@ def test_device_field_products_vs_reference(engine, ref, bits):
     assert (H[4][0] == fg).all() and (H[4][1] == gf).all(), "fd_fe_mul2"
     assert (H[5][0] == fg).all() and (H[5][1] == gf).all() and (H[5][2] == ff).all(), "fd_fe_chain3"
     assert (H[6][0] == f2).all() and (H[6][1] == g2x2).all(), "fd_fe_sqn2"
+    bad = np.nonzero((H[7][0] != fg).any(axis=1))[0]
+    assert len(bad) == 0, ("fd_o_mul (oct DSM half product)", bad[:8], H[7][0][bad[:2]], fg[bad[:2]])
 
 
 def test_device_field_products_args(engine):
     import firedancer_amd as fa
     with pytest.raises(fa.EngineError):
-        engine.debug_fe(7, np.zeros((1, 10), np.int32), np.zeros((1, 10), np.int32))
+        engine.debug_fe(8, np.zeros((1, 10), np.int32), np.zeros((1, 10), np.int32))
     assert engine.debug_fe(0, np.zeros((0, 10), np.int32), np.zeros((0, 10), np.int32)).shape == (3, 0, 10)

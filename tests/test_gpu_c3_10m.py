@@ -12,8 +12,9 @@ with the sign bit), plus the three SURVEY Q2 vectors, generated in ten
 seeded chunks of 1,000,000 (tests/golden/make_config_digests.py).
 
 Every chunk is verified under the DSM schedule the bench's throughput
-launches use (pool) and the one the C2 ring's 4096-signature batches use
-(quad), and every code of both is compared with the reference build
+launches use (pool), the one the C2 ring's 4096-signature batches use
+(quad) and the per-signature drop-in's eight-lane one (oct, forced to the
+chunk size), and every code of each is compared with the reference build
 (oracle/_ref/libfdref.so, compiled in place from /root/reference and
 shipped with the tree) and with the committed per-chunk digest of the
 reference's codes (recorded in the build container)."""
@@ -46,7 +47,7 @@ def _digest(codes):
 def test_c3_10m_adversarial_every_code_equals_reference(ref):
     spec = DIG["c3_10m"]
     e = fa.Engine(0, 1 << 20, 1 << 30, depth=1)
-    schedules = {"pool": (0, 0), "quad": (1 << 62, 1 << 62)}     # (dsm_pool_min, dsm_quad_max)
+    schedules = {"pool": (0, 0, 0), "quad": (1 << 62, 1 << 62, 0), "oct": (1 << 62, 0, 1 << 62)}   # (dsm_pool_min, dsm_quad_max, dsm_oct_max)
     total, mism, n_sigs = {}, {s: 0 for s in schedules}, 0
     cases_seen = set()
     t0 = time.time()
@@ -57,8 +58,8 @@ def test_c3_10m_adversarial_every_code_equals_reference(ref):
             exp = oracle_batch(ref, b, NTH)
             # the reference build on this box gives the codes recorded in the container
             assert _digest(exp) == spec["chunk_digests"][k], k
-            for sched, (pool_min, quad_max) in schedules.items():
-                e.dsm_pool_min, e.dsm_quad_max = pool_min, quad_max
+            for sched, (pool_min, quad_max, oct_max) in schedules.items():
+                e.dsm_pool_min, e.dsm_quad_max, e.dsm_oct_max = pool_min, quad_max, oct_max
                 got = e.verify_packed(b.blob, b.desc)
                 bad = np.nonzero(got != exp)[0]
                 mism[sched] += len(bad)
@@ -75,4 +76,4 @@ def test_c3_10m_adversarial_every_code_equals_reference(ref):
     assert n_sigs == spec["signatures"] == 10_000_003
     assert total == spec["hist"]
     assert cases_seen == set(range(len(corpus.CASES)))
-    assert mism == {"pool": 0, "quad": 0}
+    assert mism == {"pool": 0, "quad": 0, "oct": 0}

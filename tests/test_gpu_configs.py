@@ -166,17 +166,19 @@ def test_malformed_descriptors_every_path(engine, ref):
         m.close()
 
 
-@pytest.mark.parametrize("schedule", ["pool", "uniform"])
+@pytest.mark.parametrize("schedule", ["pool", "uniform", "oct"])
 def test_malformed_descriptors_schedules(ref, schedule):
-    """the pooled and uniform DSM schedules see the same ERR_ARG (the quad
-    schedule runs in test_malformed_descriptors_every_path)"""
+    """the pooled, uniform and (forced) oct DSM schedules see the same
+    ERR_ARG (the quad schedule runs in test_malformed_descriptors_every_path)"""
     b, d, exp = _malformed_case(ref, 82)
     e = fa.Engine(0, 1 << 13, 1 << 24, depth=1)
     try:
         if schedule == "pool":
             e.dsm_pool_min = 0
+        elif schedule == "oct":
+            e.dsm_pool_min, e.dsm_oct_max = 1 << 62, 1 << 62
         else:
-            e.dsm_pool_min, e.dsm_quad_max = 1 << 62, 0
+            e.dsm_pool_min, e.dsm_quad_max, e.dsm_oct_max = 1 << 62, 0, 0
         _check(e.verify_packed(b.blob, d), exp)
         e.mode = fa.MODE_PORTABLE     # portable mode reads R from the blob at the end: still no OOB read
         got = e.verify_packed(b.blob, d)

@@ -97,14 +97,14 @@ def test_pipelined_stats_attribute_setup_and_pool():
     e.close()
 
 
-def test_dsm_clock_counts_pool_and_quad_waves():
-    """fd_ed25519_gpu_dsm_clock: every pool / quad wave adds its loop's
+def test_dsm_clock_counts_pool_quad_and_oct_waves():
+    """fd_ed25519_gpu_dsm_clock: every pool / quad / oct wave adds its loop's
     shader cycles and real-time ticks; the ratio is a plausible gfx950 clock
     (the bench reports it beside the roofline)"""
     e = fa.Engine(0, 1 << 18, 1 << 29)
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev).cuda_stream
-    for n, pool_min in ((1 << 18, 0), (4096, 1 << 30)):
+    for n, pool_min in ((1 << 18, 0), (4096, 1 << 30), (64, 1 << 30)):
         b = corpus.solana_txns(n, seed=34)
         e.dsm_pool_min = pool_min
         d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
@@ -116,10 +116,11 @@ def test_dsm_clock_counts_pool_and_quad_waves():
         torch.cuda.synchronize()
         c = e.dsm_clock()
         assert (d_out.cpu().numpy() == 0).sum() >= n - 4
-        k, other = ("pool", "quad") if pool_min == 0 else ("quad", "pool")
-        assert c[k]["waves"] == (n // 128 if k == "pool" else n // 16), c
+        k = "pool" if pool_min == 0 else "quad" if n > 64 else "oct"
+        assert c[k]["waves"] == {"pool": n // 128, "quad": n // 16, "oct": n // 8}[k], c
         assert 1.0 < c[k]["ghz"] < 3.0, c
-        assert c[other]["waves"] == 0 and c[other]["ghz"] is None, c
+        for other in {"pool", "quad", "oct"} - {k}:
+            assert c[other]["waves"] == 0 and c[other]["ghz"] is None, c
     e.close()
 
 

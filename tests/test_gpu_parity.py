@@ -261,13 +261,14 @@ def test_pooled_equals_uniform(engine, pooled, n):
     b = base.tile(int(np.ceil(n / len(base))))
     b.desc = b.desc[:n]
     engine.dsm_pool_min = 1 << 62
-    engine.dsm_quad_max = 0
+    engine.dsm_quad_max = engine.dsm_oct_max = 0
     a = engine.verify_packed(b.blob, b.desc)
     p = pooled.verify_packed(b.blob, b.desc)
     assert (a == p).all(), np.nonzero(a != p)[0][:10]
     assert engine.dsm_pool_min == 1 << 62
     engine.dsm_pool_min = 262144
     engine.dsm_quad_max = 32768
+    engine.dsm_oct_max = 64
 
 
 @pytest.mark.parametrize("sizes", [(40000, 4176, 40048, 4163)])
@@ -294,7 +295,7 @@ def uniform():
     every batch"""
     e = fa.Engine(0, 1 << 18, 1 << 28)
     e.dsm_pool_min = 1 << 62
-    e.dsm_quad_max = 0
+    e.dsm_quad_max = e.dsm_oct_max = 0
     yield e
     e.close()
 
@@ -316,7 +317,11 @@ def test_quad_equals_uniform(engine, uniform, n):
     b = base.tile(int(np.ceil(n / len(base))))
     b.desc = b.desc[:n]
     assert engine.dsm_quad_max >= n
-    q = engine.verify_packed(b.blob, b.desc)
+    engine.dsm_oct_max = 0              # the quad, also for n <= 64
+    try:
+        q = engine.verify_packed(b.blob, b.desc)
+    finally:
+        engine.dsm_oct_max = 64
     u = uniform.verify_packed(b.blob, b.desc)
     assert (q == u).all(), np.nonzero(q != u)[0][:10]
 
@@ -352,5 +357,69 @@ def test_quad_q2_vectors(engine):
     vs = ed_vectors()
     b = corpus.from_triples([(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in vs])
     assert len(b) <= engine.dsm_quad_max
-    got = engine.verify_packed(b.blob, b.desc)
+    engine.dsm_oct_max = 0
+    try:
+        got = engine.verify_packed(b.blob, b.desc)
+    finally:
+        engine.dsm_oct_max = 64
     assert got.tolist() == [v["expected"] for v in vs]
+
+
+@pytest.fixture(scope="module")
+def oct():
+    """an engine that runs the eight-lane DSM (fd_k_dsm_oct, the default up
+    to 64 signatures) for every batch size"""
+    e = fa.Engine(0, 1 << 18, 1 << 28)
+    e.dsm_pool_min = 1 << 62
+    e.dsm_oct_max = 1 << 62
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("name", ["adversarial", "txn1232", "small_order", "msgsizes"])
+def test_oct_dsm_golden_corpora(oct, name):
+    b, exp = load_corpus(name)
+    got = oct.verify_packed(b.blob, b.desc)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_oct_q2_vectors_and_malleability(engine, oct):
+    """the reference-quirk (Q2) and RFC 8032 vectors and the malleability
+    KATs through the oct schedule, at its default size (one batch of at most
+    64 on the default engine) and forced"""
+    vs = ed_vectors()
+    b = corpus.from_triples([(bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["pub"])) for v in vs])
+    assert len(b) <= engine.dsm_oct_max
+    for e in (engine, oct):
+        got = e.verify_packed(b.blob, b.desc)
+        assert got.tolist() == [v["expected"] for v in vs]
+        assert got[-3:].tolist() == [-3, -3, -3]
+    m = malleability()
+    bm = corpus.from_triples([(b"Zcash", s, p) for s, p, _ in m])
+    for e in (engine, oct):
+        got = e.verify_packed(bm.blob, bm.desc)
+        for (s, p, ok), g in zip(m, got):
+            assert (g == 0) == ok
+
+
+@pytest.mark.parametrize("n", [1, 7, 9, 63, 64])
+def test_oct_equals_uniform_default_sizes(engine, uniform, n):
+    """the default engine's small batches (the oct DSM) against the uniform
+    DSM on ragged batches (n not a multiple of the 8 signatures of a wave)
+    of mixed valid / invalid signatures"""
+    base, _ = load_corpus("adversarial")
+    b = base.tile(int(np.ceil(n / len(base))))
+    b.desc = b.desc[:n]
+    assert engine.dsm_oct_max >= n
+    o = engine.verify_packed(b.blob, b.desc)
+    u = uniform.verify_packed(b.blob, b.desc)
+    assert (o == u).all(), np.nonzero(o != u)[0][:10]
+
+
+@pytest.mark.parametrize("n", [4096 + 77, 30000])
+def test_oct_equals_uniform_forced(oct, uniform, n):
+    base = corpus.adversarial(n, 200, seed=95 + n, invalid_frac=0.2)
+    o = oct.verify_packed(base.blob, base.desc)
+    u = uniform.verify_packed(base.blob, base.desc)
+    assert (o == u).all(), np.nonzero(o != u)[0][:10]

@@ -108,16 +108,20 @@ def test_gpu_strict_mode(engine, oracle):
     engine.mode = fa.MODE_STRICT
     try:
         assert engine.mode == fa.MODE_STRICT
-        # the quad (small batch), uniform and pooled DSM schedules
+        # the oct / quad (small batch), uniform and pooled DSM schedules
+        engine.dsm_oct_max = 0
         got = engine.verify_packed(b.blob, b.desc)
-        engine.dsm_quad_max = 0
+        engine.dsm_oct_max = 1 << 62
+        got_o = engine.verify_packed(b.blob, b.desc)
+        engine.dsm_oct_max, engine.dsm_quad_max = 0, 0
         got_u = engine.verify_packed(b.blob, b.desc)
         engine.dsm_pool_min = 0
         got_p = engine.verify_packed(big.blob, big.desc)
     finally:
         engine.mode = fa.MODE_AVX
         engine.dsm_quad_max = 32768
+        engine.dsm_oct_max = 64
         engine.dsm_pool_min = 262144
-    for g, e in ((got, exp), (got_u, exp), (got_p, exp_big)):
+    for g, e in ((got, exp), (got_o, exp), (got_u, exp), (got_p, exp_big)):
         bad = np.nonzero(g != e)[0]
         assert len(bad) == 0, [(int(i), int(e[i]), int(g[i])) for i in bad[:10]]

@@ -69,6 +69,7 @@ def main():
         for sch in a.schedules.split(","):
             eng.dsm_pool_min = 0 if sch == "pool" else 1 << 62
             eng.dsm_quad_max = 1 << 62 if sch == "quad" else 0
+            eng.dsm_oct_max = 1 << 62 if sch == "oct" else 0
             gots[sch] = eng.verify_packed(b.blob, b.desc)
         got = gots[a.schedules.split(",")[0]]
         t2 = time.time()

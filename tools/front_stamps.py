@@ -26,7 +26,7 @@ def main():
     L = fa.lib()
     L.fd_ed25519_gpu_front_hist.argtypes = [ctypes.c_void_p, ctypes.c_int]
     base = corpus.solana_txns(bench.UNIQUE_SIGS, seed=1000, nthreads=16)
-    h = np.zeros((4, 256), np.uint64)   # fd_front_hist[4][256]
+    h = np.zeros((6, 256), np.uint64)   # fd_front_hist[6][256]
     L.fd_ed25519_gpu_front_hist(None, 1)
     r = bench.ring_stream(fa, base, 0, nb, depth, groups=min(depth, 4), window=window)
     L.fd_ed25519_gpu_front_hist(h.ctypes.data, 0)
