@@ -1181,15 +1181,32 @@ FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
   nx += cy;
 }
 
+/* the value of lane ^ 16 (the other half of this lane's row pair): one
+   ds_swizzle_b32 in bit mode (and 0x1f, or 0, xor 0x10), through the LDS
+   crossbar without touching LDS memory.  Its latency is off the product's
+   chain: the partner limbs feed only the terms with J' >= 5, issued after
+   the swizzles' ~30 instructions of operand set-up and early terms. */
+#ifndef FD_OCT_SWIZZLE
+#define FD_OCT_SWIZZLE 1
+#endif
+FD_QDEV int32_t fd_o_partner( int32_t x ) { return __builtin_amdgcn_ds_swizzle( x, 0x401F ); }
+
 /* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9) */
 FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c ) {
   fd_oops o;
+#if FD_OCT_SWIZZLE
+#pragma unroll
+  for( int j=0; j<5; j++ ) { o.G[j] = g.v[j]; o.G[5+j] = fd_o_partner( g.v[j] ); }
+#pragma unroll
+  for( int j=0; j<5; j++ ) fd_o_both( f.v[j], o.F[j], o.F[5+j] );
+#else
 #pragma unroll
   for( int j=0; j<5; j++ ) {
     fd_o_both( f.v[j], o.F[j], o.F[5+j] );
     int32_t a, b; fd_o_both( g.v[j], a, b );
     o.G[j] = g.v[j]; o.G[5+j] = (int32_t)fd_sel( c.hm, (uint32_t)a, (uint32_t)b );
   }
+#endif
 #pragma unroll
   for( int i=1; i<10; i+=2 ) {
     o.FA[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sA) );
