@@ -284,14 +284,18 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   for( int j=0; j<8; j++ ) dig[j] = fd_bswap64( dig[j] );
   uint64_t k[4];
 #ifdef FD_FRONT_STAMPS
-  unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+  /* stamps pinned by data dependences (the builtin alone is scheduled
+     freely: it read sc_reduce as 0.1 us) */
+  unsigned long long ts1;
+  asm volatile( "s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts1) : "v"((uint32_t)dig[0]), "v"((uint32_t)dig[7]) : "memory" );
 #endif
   fd_sc_reduce( k, dig );
   uint32_t kw[8];
 #pragma unroll
   for( int j=0; j<4; j++ ) { kw[2*j] = (uint32_t)k[j]; kw[2*j+1] = (uint32_t)(k[j] >> 32); }
 #ifdef FD_FRONT_STAMPS
-  unsigned long long ts2 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long ts2;
+  asm volatile( "s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts2) : "v"(kw[0]), "v"(kw[7]) : "memory" );
 #endif
   int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
 #pragma unroll
@@ -299,7 +303,9 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
 #ifdef FD_FRONT_STAMPS
   {
-    unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long ts3;
+    int const os = op_start[i];
+    asm volatile( "s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts3) : "v"(os) : "memory" );
     unsigned b4 = (unsigned)((ts2 - ts1) / 20ULL), b5 = (unsigned)((ts3 - ts2) / 20ULL);
     atomicAdd( &fd_front_hist[4][b4 > 255u ? 255u : b4], 1ULL );
     atomicAdd( &fd_front_hist[5][b5 > 255u ? 255u : b5], 1ULL );
@@ -1274,6 +1280,28 @@ FD_QDEV void fd_fh_full( fe & v, fh const & x ) {
   for( int j=0; j<5; j++ ) fd_o_both( x.v[j], v.v[j], v.v[5+j] );
 }
 
+/* the quad's lane mixes (fd_q_subadd12 / fd_q_submix / fd_q_dblmix) on
+   half field elements: every one is limb by limb */
+FD_QDEV void fd_h_subadd12( fh & x, uint32_t m12, uint32_t s1 ) {
+  fh p; fd_fh_qperm<FD_QP(0,2,1,3)>( p, x );
+#pragma unroll
+  for( int k=0; k<5; k++ ) x.v[k] = (int32_t)((uint32_t)x.v[k] + fd_qterm( (uint32_t)p.v[k], m12, s1 ));
+}
+FD_QDEV void fd_h_submix( fh & x, uint32_t sh, uint32_t se ) {
+  fh u, w; fd_fh_qperm<FD_QP(2,2,0,0)>( u, x ); fd_fh_qperm<FD_QP(1,1,3,3)>( w, x );
+#pragma unroll
+  for( int k=0; k<5; k++ ) x.v[k] = (int32_t)(((uint32_t)u.v[k] << sh) + fd_qterm( (uint32_t)w.v[k], ~0u, se ));
+}
+FD_QDEV void fd_h_dblmix( fh & x, uint32_t m03, uint32_t s02 ) {
+  fh b, c; fd_fh_qperm<FD_QP(1,1,1,1)>( b, x ); fd_fh_qperm<FD_QP(2,2,2,2)>( c, x );
+#pragma unroll
+  for( int k=0; k<5; k++ )
+    x.v[k] = (int32_t)(((uint32_t)x.v[k] & m03) + fd_qterm( (uint32_t)b.v[k], ~0u, m03 ) + fd_qterm( (uint32_t)c.v[k], ~0u, s02 ));
+}
+FD_QDEV void fd_o_tab_store( int32_t * p, fh const & x ) {
+  ((int4 *)p)[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); ((int4 *)p)[1] = make_int4( x.v[4], 0, 0, 0 );
+}
+
 struct fd_oct_lds {
   int32_t tab[FD_OSIGS+1][8*FD_OTAB_ENTRY];   /* Ai per signature, [FD_OSIGS] = Bi */
   uint8_t ops[FD_OSIGS][FD_QOPS_ROW];
@@ -1333,38 +1361,33 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
   fd_octc const oc = fd_octc_make( h );
 
-  /* Ai = {A,3A,...,15A}: the quad's prologue on whole field elements
-     (both halves compute it), each lane storing its half */
+  /* Ai = {A,3A,...,15A}: the quad's prologue (avx/fd_ed25519_ge.c:423-481)
+     on half field elements, each lane storing its half of every entry */
   fe one; fd_fe_set( one, 1 );
-  fe d111 = q==3u ? FD_GPU_D2 : one;
+  fh const d111 = fd_fh_own( q==3u ? FD_GPU_D2 : one, oc.hm );
   int32_t * tab_s = L.tab[ls] + q*FD_OTAB_LANE + 8u*h;
-  fe vu, vt, f, g;
-  FD_QMUL( vu, r, d111 ); fd_q_subadd12( vu, m12, mq1 );
+  fh ra = fd_fh_own( r, oc.hm ), vu, va, f0, g0;
+  fd_o_mul( vu, ra, d111, oc ); fd_h_subadd12( vu, m12, mq1 );
+  fd_o_tab_store( tab_s, vu );
   {
-    fh x = fd_fh_own( vu, oc.hm );
-    ((int4 *)tab_s)[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); ((int4 *)tab_s)[1] = make_int4( x.v[4], 0, 0, 0 );
-  }
-  {
-    fe a, b; fd_fe_qperm<FD_QP(2,1,2,0)>( a, r ); fd_fe_qperm<FD_QP(1,1,1,1)>( b, r );
+    fh a, b; fd_fh_qperm<FD_QP(2,1,2,0)>( a, ra ); fd_fh_qperm<FD_QP(1,1,1,1)>( b, ra );
 #pragma unroll
-    for( int k=0; k<10; k++ ) {
-      f.v[k] = (int32_t)((uint32_t)a.v[k] + ((uint32_t)b.v[k] & mq0));
-      g.v[k] = (int32_t)((uint32_t)f.v[k] << (q==3u ? 1 : 0));
+    for( int k=0; k<5; k++ ) {
+      f0.v[k] = (int32_t)((uint32_t)a.v[k] + ((uint32_t)b.v[k] & mq0));
+      g0.v[k] = (int32_t)((uint32_t)f0.v[k] << (q==3u ? 1 : 0));
     }
-    FD_QMUL( vt, f, g );
-    fd_q_dblmix( vt, m03, s02 );
+    fd_o_mul( va, f0, g0, oc );
+    fd_h_dblmix( va, m03, s02 );
   }
-  fd_fe_qperm<FD_QP(3,2,3,1)>( f, vt ); fd_fe_qperm<FD_QP(2,1,0,0)>( g, vt );
-  FD_QMUL( r, f, g ); fd_q_subadd12( r, m12, mq1 );
+  fd_fh_qperm<FD_QP(3,2,3,1)>( f0, va ); fd_fh_qperm<FD_QP(2,1,0,0)>( g0, va );
+  fd_o_mul( ra, f0, g0, oc ); fd_h_subadd12( ra, m12, mq1 );
   for( int e=0; e<7; e++ ) {
-    FD_QMUL( vt, r, vu );
-    fd_q_submix( vt, q >> 1, (q & 1u) ? 0u : ~0u );
-    fd_fe_qperm<FD_QP(2,3,2,1)>( f, vt ); fd_fe_qperm<FD_QP(3,1,0,0)>( g, vt );
-    FD_QMUL( vt, f, g );
-    FD_QMUL( vu, vt, d111 ); fd_q_subadd12( vu, m12, mq1 );
-    fh x = fd_fh_own( vu, oc.hm );
-    int4 * p = (int4 *)(tab_s + (e+1)*FD_OTAB_ENTRY);
-    p[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); p[1] = make_int4( x.v[4], 0, 0, 0 );
+    fd_o_mul( va, ra, vu, oc );
+    fd_h_submix( va, q >> 1, (q & 1u) ? 0u : ~0u );
+    fd_fh_qperm<FD_QP(2,3,2,1)>( f0, va ); fd_fh_qperm<FD_QP(3,1,0,0)>( g0, va );
+    fd_o_mul( va, f0, g0, oc );
+    fd_o_mul( vu, va, d111, oc ); fd_h_subadd12( vu, m12, mq1 );
+    fd_o_tab_store( tab_s + (e+1)*FD_OTAB_ENTRY, vu );
   }
   __syncthreads();
 
@@ -1425,6 +1448,7 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
 
   /* the whole final state, then the quad's final p1p1 -> p2 and the limb
      compare (Q2) */
+  fe vt, f, g;
   fd_fh_full( vt, s );
   fe P2;
   fd_fe_qperm<FD_QP(0,1,2,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
