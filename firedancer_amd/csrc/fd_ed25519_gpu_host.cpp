@@ -116,6 +116,7 @@ struct fd_ed25519_gpu_slot {
   uint8_t *               h_blob;
   fd_ed25519_gpu_desc_t * h_desc;
   int32_t *               h_out;
+  int32_t *               h_out_dev;  /* h_out as the device addresses it (coherent, mapped), or NULL */
   /* device */
   uint8_t *               d_blob;
   fd_ed25519_gpu_desc_t * d_desc;
@@ -142,6 +143,7 @@ struct fd_ed25519_gpu {
   unsigned long pool_min; /* batches >= this take the pooled DSM */
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long oct_max;  /* and batches <= this the eight-lane DSM */
+  unsigned long out_direct_max;  /* ring batches <= this get their codes written to pinned memory by the DSM */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
@@ -252,6 +254,10 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->pool_min = FD_DSM_POOL_MIN_DEFAULT;
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->oct_max  = FD_DSM_OCT_MAX_DEFAULT;
+  {
+    char const * od = getenv( "FD_ED25519_GPU_OUT_DIRECT_MAX" );   /* A/B: 0 = always the D2H copy */
+    g->out_direct_max = od ? strtoul( od, NULL, 0 ) : 65536UL;
+  }
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );
   { char const * ga = getenv( "FD_ED25519_GPU_GROUP_ALWAYS" ); g->group_always = ga && atoi( ga ); }  /* experiments */
@@ -266,7 +272,10 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     HIPCHK( hipHostMalloc( (void **)&sl->h_blob, blob_cap, hipHostMallocDefault ) );
     HIPCHK( hipHostMalloc( (void **)&sl->h_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t), hipHostMallocDefault ) );
-    HIPCHK( hipHostMalloc( (void **)&sl->h_out,  max_sigs * sizeof(int32_t), hipHostMallocDefault ) );
+    /* codes of small batches are written by the kernels straight into
+       h_out (fine-grained, mapped: no D2H copy, fd_slot_enqueue_) */
+    HIPCHK( hipHostMalloc( (void **)&sl->h_out,  max_sigs * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent ) );
+    if( hipHostGetDevicePointer( (void **)&sl->h_out_dev, sl->h_out, 0 ) != hipSuccess ) { (void)hipGetLastError(); sl->h_out_dev = NULL; }
     HIPCHK( hipMalloc( (void **)&sl->d_blob, blob_cap ) );
     HIPCHK( hipMemset( sl->d_blob, 0, blob_cap ) );
     HIPCHK( hipMalloc( (void **)&sl->d_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t) ) );
@@ -748,9 +757,15 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );
   fd_ed25519_gpu_desc_t const * dd = (fd_ed25519_gpu_desc_t const *)(sl->d_blob + doff);
-  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, sl->d_out, st, g->mode, g->pool_min, g->quad_max, g->oct_max )) != hipSuccess )
+  /* up to out_direct_max signatures the DSM writes its codes into the
+     slot's pinned h_out itself: no D2H copy (a blit kernel and its gap,
+     ~5 us of every small batch's round trip); they are visible to the
+     host once the slot's done event completes */
+  int odirect = sl->h_out_dev && n <= g->out_direct_max;
+  if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, odirect ? sl->h_out_dev : sl->d_out, st,
+                                  g->mode, g->pool_min, g->quad_max, g->oct_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
-  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
+  if( !odirect && (e = hipMemcpyAsync( sl->h_out, sl->d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, st )) != hipSuccess )
     return fd_gpu_fail( "D2H out", e );
   if( (e = hipEventRecord( sl->done, st )) != hipSuccess ) return fd_gpu_fail( "event", e );
   sl->n = n;

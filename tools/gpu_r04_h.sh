@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4, session H: the whole GPU suite on the current tree (incl. the
+# 10M C3 corpus under pool, quad and oct), smoke, the per-signature
+# latency with small-batch codes written straight to pinned memory, the
+# bench and its kernel-trace profile.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo GPU TESTS FAILED; grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -30; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
+timeout -k 10 300 ./tools/build/per_sig_threads 2000 > gpurun_out/per_sig_h.jsonl 2> gpurun_out/per_sig_h.err || { echo PERSIG FAILED; tail -20 gpurun_out/per_sig_h.err; exit 1; }
+cat gpurun_out/per_sig_h.jsonl
+timeout -k 10 400 python3 -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -30 gpurun_out/bench.err; exit 1; }
+cut -c1-400 gpurun_out/bench.json
+R=$GRAFT_REPO_ROOT
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --no-latency > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err ) || { echo PROF FAILED; tail -30 gpurun_out/prof.err; exit 1; }
+head -4 gpurun_out/prof/run_kernel_stats.csv | cut -c1-200
