@@ -191,8 +191,14 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
     int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
 #pragma unroll
     for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
-    op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
-  } else op_start[i] = fd_recode( sw, kw, ops + i, n );
+  }
+  /* the two-pass recoder, S's digits parked in this lane's slots of the
+     wave's SHA-512 stage (free once the digest is out) */
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  static_assert( FD_SHA_STAGE_BYTES >= FD_RECODE2_SLOTS*64*sizeof(uint16_t), "recoder slots fit the stage" );
+  lds_u16 * slots = (lds_u16 *)(sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES) + (threadIdx.x & 63u);
+  op_start[i] = sigmajor ? fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, slots, 64u )
+                         : fd_recode2( sw, kw, ops + i, n, slots, 64u );
 }
 
 /* fd_prep_body on a wave pair (the latency path's front end, fd_k_front):
@@ -300,7 +306,12 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
 #pragma unroll
   for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
-  op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
+  /* the two-pass recoder: S's digits parked in this lane's slots of the
+     chunk ring (its last chunk was consumed above; the schedule wave has
+     exited) */
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  static_assert( sizeof(fd_sha2_ring) >= FD_RECODE2_SLOTS*64*sizeof(uint16_t), "recoder slots fit the chunk ring" );
+  op_start[i] = fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, (lds_u16 *)ring + (threadIdx.x & 63u), 64u );
 #ifdef FD_FRONT_STAMPS
   {
     unsigned long long ts3;

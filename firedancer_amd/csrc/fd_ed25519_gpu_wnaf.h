@@ -128,4 +128,51 @@ FD_DEV int fd_recode( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t 
   return FD_OPS_MAX - 256 - cnt;
 }
 
+/* The same stream in two passes (the latency front end, fd_prep2_body,
+   which has LDS for it): S's digits first, each as (bit << 8 | op) in the
+   lane's slots of buf (buf[i*bstride], i < FD_RECODE2_SLOTS), then k's
+   digits, each preceded by S's digits at or below its bit.  The merged
+   loop above exchanges its two recoding registers (9 values each) at
+   every change of scalar, about every other digit; here each scalar keeps
+   its registers.  A pending S is below L < 2^253, whose width-5 digits are
+   at least 5 bits apart: at most 51 of them.  The front end parks them in
+   its SHA-512 chunk ring, which is free once the round wave has consumed
+   the last chunk (8 KiB = 64 slots x 64 lanes). */
+#define FD_RECODE2_SLOTS 64
+template<typename BUF>   /* uint16_t * (host), or an LDS (address space 3) pointer */
+FD_DEV int fd_recode2( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t * ops, uint64_t stride,
+                       BUF buf, uint32_t bstride ) {
+  fd_wn v;
+  fd_wn_init( v, sw );
+  int ns = 0;
+  while( v.pos != FD_WN_DONE && ns < FD_RECODE2_SLOTS ) {
+    int b = v.pos;
+    if( b > 255 ) break;
+    int dg = fd_wn_step( v );
+    buf[(uint32_t)ns*bstride] = (uint16_t)(((uint32_t)b << 8) | fd_op_enc( 1, dg ));
+    ns++;
+  }
+  int cnt = 0, si = 0, nk = 0;
+  uint32_t nx = ns ? (uint32_t)buf[0] : 0x10000u;     /* S's next digit; 0x10000: none left */
+  fd_wn_init( v, kw );
+  while( v.pos != FD_WN_DONE && nk < 128 ) {
+    int b = v.pos;
+    if( b > 255 ) break;
+    while( (int)(nx >> 8) <= b ) {                     /* S first at a shared bit (it is the later op) */
+      ops[(uint64_t)(FD_OPS_MAX - 1 - ((int)(nx >> 8) + cnt))*stride] = (uint8_t)nx;
+      cnt++; si++;
+      nx = si < ns ? (uint32_t)buf[(uint32_t)si*bstride] : 0x10000u;
+    }
+    int dg = fd_wn_step( v );
+    ops[(uint64_t)(FD_OPS_MAX - 1 - (b + cnt))*stride] = fd_op_enc( 0, dg );
+    cnt++; nk++;
+  }
+  while( nx < 0x10000u ) {
+    ops[(uint64_t)(FD_OPS_MAX - 1 - ((int)(nx >> 8) + cnt))*stride] = (uint8_t)nx;
+    cnt++; si++;
+    nx = si < ns ? (uint32_t)buf[(uint32_t)si*bstride] : 0x10000u;
+  }
+  return FD_OPS_MAX - 256 - cnt;
+}
+
 #endif /* FD_ED25519_GPU_WNAF_H */

@@ -19,6 +19,18 @@ void h_recode( uint8_t * ops, int * op_start, uint8_t const * s, uint8_t const *
     op_start[i] = fd_recode( sw, kw, ops + i*FD_OPS_MAX, 1 );
   }
 }
+/* the two-pass recoder (fd_recode2, the latency front end's) */
+void h_recode2( uint8_t * ops, int * op_start, uint8_t const * s, uint8_t const * k, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    uint32_t sw[8], kw[8];
+    uint16_t buf[FD_RECODE2_SLOTS];
+    for( int j=0; j<8; j++ ) {
+      sw[j] = (uint32_t)s[32*i+4*j] | ((uint32_t)s[32*i+4*j+1]<<8) | ((uint32_t)s[32*i+4*j+2]<<16) | ((uint32_t)s[32*i+4*j+3]<<24);
+      kw[j] = (uint32_t)k[32*i+4*j] | ((uint32_t)k[32*i+4*j+1]<<8) | ((uint32_t)k[32*i+4*j+2]<<16) | ((uint32_t)k[32*i+4*j+3]<<24);
+    }
+    op_start[i] = fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, buf, 1 );
+  }
+}
 void h_fe_mul( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
   for( unsigned long i=0; i<n; i++ ) {
     fd_gpu_fe_t a, b, c;

@@ -51,8 +51,12 @@ def test_recode_vs_oracle_slide(harness, oracle):  # noqa: F811
     K = np.frombuffer(b"".join(k.to_bytes(32, "little") for _, k in pairs), np.uint8).copy()
     ops = np.zeros((n, FD_OPS_MAX), np.uint8)
     start = np.zeros(n, np.int32)
-    harness.h_recode(P(ops), P(start), P(S), P(K), ctypes.c_ulong(n))
-    for i, (s, k) in enumerate(pairs):
-        exp, st = expected_stream(oracle, s, k)
-        assert start[i] == st, (i, s, k)
-        assert (ops[i] == exp).all(), (i, s, k, np.nonzero(ops[i] != exp)[0][:8])
+    # the merged recoder (throughput prep) and the two-pass one (latency front end)
+    for fn in (harness.h_recode, harness.h_recode2):
+        ops = np.zeros((n, FD_OPS_MAX), np.uint8)
+        start = np.zeros(n, np.int32)
+        fn(P(ops), P(start), P(S), P(K), ctypes.c_ulong(n))
+        for i, (s, k) in enumerate(pairs):
+            exp, st = expected_stream(oracle, s, k)
+            assert start[i] == st, (fn, i, s, k)
+            assert (ops[i] == exp).all(), (fn, i, s, k, np.nonzero(ops[i] != exp)[0][:8])
