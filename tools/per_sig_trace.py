@@ -38,9 +38,12 @@ def calls(n):
 
 
 def timeline(d):
-    """per-call breakdown from a rocprofv3 kernel trace: a call's H2D and
-    D2H are blit kernels (__amd_rocclr_copyBuffer) on the slot's stream, so
-    each call is the sequence copy, fd_k_front, fd_k_dsm_quad, copy"""
+    """per-call breakdown from a rocprofv3 kernel trace: a call's H2D is a
+    blit kernel (__amd_rocclr_copyBuffer) on the slot's stream, then
+    fd_k_front and the DSM (fd_k_dsm_oct since round 4; the codes are
+    written straight into the slot's pinned memory, so no D2H copy
+    follows: a trace from before that shows a second copy, reported as
+    d2h_blit_us)"""
     ev = []
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -48,19 +51,25 @@ def timeline(d):
     ev.sort()
     rows = []
     for i in range(2, len(ev) - 2):
-        if "copy" in ev[i-1][2] and "front" in ev[i][2] and "dsm" in ev[i+1][2] and "copy" in ev[i+2][2]:
+        if "copy" in ev[i-1][2] and "front" in ev[i][2] and "dsm" in ev[i+1][2]:
             c, f, q, o = ev[i-1], ev[i], ev[i+1], ev[i+2]
-            rows.append([c[1] - c[0], f[0] - c[1], f[1] - f[0], max(q[0] - f[1], 0), q[1] - q[0],
-                         max(o[0] - q[1], 0), o[1] - o[0], o[1] - c[0], c[0] - ev[i-2][1]])
+            nxt = ev[i+3][2] if i + 3 < len(ev) else ""
+            d2h = o[1] - o[0] if ("copy" in o[2] and "front" not in nxt) else 0   # o is the next call's H2D when a front follows it
+            end = o[1] if d2h else q[1]
+            rows.append([c[1] - c[0], f[0] - c[1], f[1] - f[0], max(q[0] - f[1], 0), q[1] - q[0], d2h, end - c[0],
+                         c[0] - ev[i-2][1], q[2]])
     if not rows:
         return None
-    a = np.array(rows, dtype=np.float64) / 1e3
-    names = ["h2d_blit_us", "h2d_to_front_us", "fd_k_front_us", "front_to_dsm_us", "fd_k_dsm_quad_us",
-             "dsm_to_d2h_us", "d2h_blit_us", "device_span_us", "idle_between_calls_us"]
+    kern = sorted(set(r[-1] for r in rows))
+    a = np.array([r[:-1] for r in rows], dtype=np.float64) / 1e3
+    names = ["h2d_blit_us", "h2d_to_front_us", "fd_k_front_us", "front_to_dsm_us", "dsm_us",
+             "d2h_blit_us", "device_span_us", "idle_before_call_us"]
     # the calls run in message-size order: the first half C2-shaped, the second short
     h = len(a) // 2
-    return {label: {"calls": len(x), **{n: round(float(np.median(x[:, c])), 1) for c, n in enumerate(names)}}
-            for label, x in (("c2_1103_1167B", a[1:h]), ("short_200B", a[h + 1:]))}
+    out = {label: {"calls": len(x), **{n: round(float(np.median(x[:, c])), 1) for c, n in enumerate(names)}}
+           for label, x in (("c2_1103_1167B", a[1:h]), ("short_200B", a[h + 1:]))}
+    out["dsm_kernels"] = kern
+    return out
 
 
 if __name__ == "__main__":
