@@ -332,7 +332,9 @@ class Engine:
         if clear:
             return None
         def one(w, c, t):
-            return {"waves": int(w), "ghz": (0.1 * float(c) / float(t)) if t else None}
+            return {"waves": int(w), "ghz": (0.1 * float(c) / float(t)) if t else None,
+                    "cycles_per_wave": float(c) / float(w) if w else None,
+                    "us_per_wave": 0.01 * float(t) / float(w) if w else None}
         return {"pool": one(*out[0:3]), "quad": one(*out[3:6]), "oct": one(*out[6:9])}
 
     def submit(self, blob: np.ndarray, desc: np.ndarray) -> int:

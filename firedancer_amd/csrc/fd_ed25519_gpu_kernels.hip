@@ -1202,16 +1202,33 @@ FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
    ds_swizzle_b32 in bit mode (and 0x1f, or 0, xor 0x10), through the LDS
    crossbar without touching LDS memory.  Its latency is off the product's
    chain: the partner limbs feed only the terms with J' >= 5, issued after
-   the swizzles' ~30 instructions of operand set-up and early terms. */
+   the swizzles' ~30 instructions of operand set-up and early terms.
+   FD_OCT_SWIZZLE: 0 = g's partner limbs by permlane copy/swap/select, 1 =
+   by swizzle, 2 = by swizzle, sent pre-scaled by the receiver's J' >= 5
+   factor.  Main-loop cycles per single-signature wave, 2 rounds on one
+   box: 697,845 / 685,876 / 674,928 (profiles/r04_oct_exchange_ab.jsonl). */
 #ifndef FD_OCT_SWIZZLE
-#define FD_OCT_SWIZZLE 1
+#define FD_OCT_SWIZZLE 2
 #endif
 FD_QDEV int32_t fd_o_partner( int32_t x ) { return __builtin_amdgcn_ds_swizzle( x, 0x401F ); }
 
 /* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9) */
 FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c ) {
   fd_oops o;
-#if FD_OCT_SWIZZLE
+#if FD_OCT_SWIZZLE == 2
+  /* the partner limbs only ever enter J' >= 5 terms, always scaled by this
+     lane's m19: the partner sends them scaled for us (h = 1 sends 19 g,
+     h = 0 sends g), so the swizzle results feed the MACs directly */
+#pragma unroll
+  for( int j=0; j<5; j++ ) {
+    o.G[j] = g.v[j];
+    int32_t const t19 = fd_opaque( (int32_t)(19u * (uint32_t)g.v[j]) );
+    if( j ) o.G19[j] = t19;
+    o.G19[5+j] = fd_o_partner( (int32_t)fd_sel( c.hm, (uint32_t)t19, (uint32_t)g.v[j] ) );
+  }
+#pragma unroll
+  for( int j=0; j<5; j++ ) fd_o_both( f.v[j], o.F[j], o.F[5+j] );
+#elif FD_OCT_SWIZZLE
 #pragma unroll
   for( int j=0; j<5; j++ ) { o.G[j] = g.v[j]; o.G[5+j] = fd_o_partner( g.v[j] ); }
 #pragma unroll
@@ -1230,10 +1247,12 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
     o.FB[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sB) );
   }
   o.G19[0] = 0;
+#if FD_OCT_SWIZZLE != 2
 #pragma unroll
   for( int j=1; j<5; j++ )  o.G19[j] = fd_opaque( (int32_t)(19u   * (uint32_t)o.G[j]) );
 #pragma unroll
   for( int j=5; j<10; j++ ) o.G19[j] = fd_opaque( (int32_t)(c.m19 * (uint32_t)o.G[j]) );
+#endif
 
   int64_t S[5];
   S[0] = fd_opaque64( (int64_t)c.bE ); S[1] = fd_opaque64( (int64_t)c.bO ); S[2] = fd_opaque64( (int64_t)c.bE );

@@ -3,6 +3,8 @@
 single-signature calls (the eight-lane DSM) one after another, and lone
 4,096-signature batches (the quad DSM), each on an otherwise idle device.
 Separates the per-signature latency's clock from its instruction count.
+Variant libraries (FD_ED25519_LIB) A/B the oct DSM's main loop by its
+cycles per wave (one wave per single-signature call).
 usage: oct_clock.py [calls]"""
 import json
 import os
@@ -35,7 +37,8 @@ def main():
             t.append(time.perf_counter() - t0)
         c = e.dsm_clock()
         k = "oct" if n <= e.dsm_oct_max else "quad"
-        out[name] = {"kernel": k, "waves": c[k]["waves"], "ghz": c[k]["ghz"], "call_p50_ms": float(np.median(t) * 1e3),
+        out[name] = {"kernel": k, "waves": c[k]["waves"], "ghz": c[k]["ghz"], "loop_cycles_per_wave": c[k]["cycles_per_wave"],
+                     "loop_us_per_wave": c[k]["us_per_wave"], "call_p50_ms": float(np.median(t) * 1e3),
                      "accepted": int((got == 0).sum())}
     print(json.dumps(out), flush=True)
     e.close()
