@@ -1185,13 +1185,6 @@ template<int J, int JP> FD_QDEV int64_t fd_o_term( fd_oops const & o, int64_t ac
   int32_t const go = (JP <= J) ? o.G[JP] : o.G19[JP];
   return fd_mad( fo, go, acc );
 }
-/* slot J's whole column sum from acc (one serial chain of 10 MACs) */
-template<int J> FD_QDEV int64_t fd_o_col( fd_oops const & o, int64_t acc ) {
-  acc = fd_o_term<J,0>( o, acc ); acc = fd_o_term<J,1>( o, acc ); acc = fd_o_term<J,2>( o, acc ); acc = fd_o_term<J,3>( o, acc );
-  acc = fd_o_term<J,4>( o, acc ); acc = fd_o_term<J,5>( o, acc ); acc = fd_o_term<J,6>( o, acc ); acc = fd_o_term<J,7>( o, acc );
-  acc = fd_o_term<J,8>( o, acc ); acc = fd_o_term<J,9>( o, acc );
-  return acc;
-}
 template<int JP> FD_QDEV void fd_o_terms( fd_oops const & o, int64_t (&S)[5] ) {
   S[0] = fd_o_term<0,JP>( o, S[0] ); S[1] = fd_o_term<1,JP>( o, S[1] ); S[2] = fd_o_term<2,JP>( o, S[2] );
   S[3] = fd_o_term<3,JP>( o, S[3] ); S[4] = fd_o_term<4,JP>( o, S[4] );
@@ -1214,9 +1207,6 @@ FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
    by swizzle, 2 = by swizzle, sent pre-scaled by the receiver's J' >= 5
    factor.  Main-loop cycles per single-signature wave, 2 rounds on one
    box: 697,845 / 685,876 / 674,928 (profiles/r04_oct_exchange_ab.jsonl). */
-#ifndef FD_OCT_CHAIN
-#define FD_OCT_CHAIN 0
-#endif
 #ifndef FD_OCT_SWIZZLE
 #define FD_OCT_SWIZZLE 2
 #endif
@@ -1266,24 +1256,6 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
 
   int64_t S[5];
   uint64_t const hm64 = ((uint64_t)c.hm << 32) | c.hm;
-#if FD_OCT_CHAIN
-  /* the chain absorbed into the column sums (as fd_fe_chain does for a
-     whole product): slot 4 first and its first carry across (A), then
-     every later slot STARTS from its bias plus the carry into it, so no
-     serial run of 64-bit shifts and adds is left after the MACs; the
-     sums are the same integers, added in another order */
-  S[4] = fd_o_col<4>( o, fd_opaque64( (int64_t)c.bE ) );
-  {
-    int64_t cy = S[4] >> c.wE;
-    S[4] = fd_sel64( c.hm, S[4], (int64_t)(uint64_t)((uint32_t)S[4] & c.mE) );
-    int64_t a, b; fd_o_both64( cy, a, b );
-    S[0] = fd_o_col<0>( o, fd_opaque64( (int64_t)c.bE + (int64_t)((uint64_t)a & hm64) ) );
-  }
-  { int64_t cy = S[0] >> c.wE; S[0] = (int64_t)(uint64_t)((uint32_t)S[0] & c.mE); S[1] = fd_o_col<1>( o, fd_opaque64( (int64_t)c.bO + cy ) ); }
-  { int64_t cy = S[1] >> c.wO; S[1] = (int64_t)(uint64_t)((uint32_t)S[1] & c.mO); S[2] = fd_o_col<2>( o, fd_opaque64( (int64_t)c.bE + cy ) ); }
-  { int64_t cy = S[2] >> c.wE; S[2] = (int64_t)(uint64_t)((uint32_t)S[2] & c.mE); S[3] = fd_o_col<3>( o, fd_opaque64( (int64_t)c.bO + cy ) ); }
-  fd_o_carry( S[3], S[4], c.wO, c.mO );
-#else
   S[0] = fd_opaque64( (int64_t)c.bE ); S[1] = fd_opaque64( (int64_t)c.bO ); S[2] = fd_opaque64( (int64_t)c.bE );
   S[3] = fd_opaque64( (int64_t)c.bO ); S[4] = fd_opaque64( (int64_t)c.bE );
   fd_o_terms<0>( o, S ); fd_o_terms<1>( o, S ); fd_o_terms<2>( o, S ); fd_o_terms<3>( o, S ); fd_o_terms<4>( o, S );
@@ -1292,7 +1264,11 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
   /* the reference's chain 0,4,1,5,2,6,3,7,4,8,9,0 (fd_fe_carry) as
      A: c4 (h = 0's slot 4) into limb 5; B-E: 0->1 | 5->6 ... 3->4 | 8->9 in
      both halves at once; F: c4' into limb 5 and 19 c9 into limb 0 across;
-     G: c0' (h = 0) */
+     G: c0' (h = 0).  Absorbing the carries into the next slot's column
+     sum (each slot's 10 MACs then one dependent chain) measured 13 % more
+     loop cycles: 758.7 K against 672.2 K per signature
+     (profiles/r04_oct_chain_ab.jsonl) -- five interleaved columns keep a
+     dependent MAC five issues away, a serial chain waits on each. */
   {
     int64_t cy = S[4] >> c.wE;
     S[4] = fd_sel64( c.hm, S[4], (int64_t)(uint64_t)((uint32_t)S[4] & c.mE) );
@@ -1303,7 +1279,6 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
   fd_o_carry( S[1], S[2], c.wO, c.mO );
   fd_o_carry( S[2], S[3], c.wE, c.mE );
   fd_o_carry( S[3], S[4], c.wO, c.mO );
-#endif
   {
     int64_t cy = S[4] >> c.wE;
     S[4] = (int64_t)(uint64_t)((uint32_t)S[4] & c.mE);
