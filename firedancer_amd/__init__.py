@@ -98,6 +98,8 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_submit.restype = ip
         L.fd_ed25519_gpu_try_submit.argtypes = [vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fd_ed25519_gpu_try_submit.restype = ip
+        L.fd_ed25519_gpu_try_submit2.argtypes = [vp, ul, vp, ul, vp, ul, vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fd_ed25519_gpu_try_submit2.restype = ip
         L.fd_ed25519_gpu_feeder_synth.argtypes = [vp, vp, ul, vp, ul, ul, vp, ul, ul, ip, ul, vp, vp]
         L.fd_ed25519_gpu_feeder_synth.restype = ip
         L.fd_ed25519_gpu_poll.argtypes = [vp, ul, vp, ip]
@@ -491,7 +493,7 @@ class Job(ctypes.Structure):
     _fields_ = [("n", ctypes.c_ulong), ("blob", ctypes.c_void_p), ("blob_sz", ctypes.c_ulong),
                 ("desc", ctypes.c_void_p), ("out", ctypes.c_void_p), ("state", ctypes.c_int),
                 ("t_push_ns", ctypes.c_ulong), ("t_submit_ns", ctypes.c_ulong), ("t_done_ns", ctypes.c_ulong),
-                ("t_pick_ns", ctypes.c_ulong)]
+                ("t_pick_ns", ctypes.c_ulong), ("blob2", ctypes.c_void_p), ("blob2_sz", ctypes.c_ulong)]
 
 
 # fd_ed25519_gpu_synth_stat_t

@@ -109,6 +109,17 @@ static void fd_job_finish( fd_ed25519_gpu_job_t * j, int state ) {
 
 /* stage + submit one job; 1 submitted, 0 ring full (retry later), < 0 the job failed (finished) */
 static int fd_feeder_submit( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
+  if( j->blob2_sz ) {
+    /* two pieces (an in-place batch across a ring wrap): submitted as
+       given, the descriptors index the concatenation */
+    unsigned long ticket = 0;
+    int r = fd_ed25519_gpu_try_submit2( f->gpu, j->n, j->blob, j->blob_sz, j->blob2, j->blob2_sz, j->desc, &ticket );
+    if( !r ) return 0;
+    if( r < 0 ) { fd_job_finish( j, r ); return -1; }
+    j->t_submit_ns = fd_feeder_now();
+    f->inflight.push_back( fd_feeder_inflight{ j, ticket } );
+    return 1;
+  }
   unsigned long n = j->n, b0, b1;
   fd_ed25519_desc_span( n, j->desc, j->blob_sz, &b0, &b1 );
   if( b1 - b0 > f->max_blob ) { fd_job_finish( j, FD_ED25519_ERR_ARG ); return -1; }
@@ -252,7 +263,7 @@ FD_EXPORT int fd_ed25519_gpu_device_numa_node( int device ) {
 FD_EXPORT int fd_ed25519_gpu_feeder_numa_node( fd_ed25519_gpu_feeder_t const * f ) { return f ? f->numa_node : -1; }
 
 FD_EXPORT int fd_ed25519_gpu_feeder_push( fd_ed25519_gpu_feeder_t * f, fd_ed25519_gpu_job_t * j ) {
-  if( !f || !j || j->n > f->max_sigs || (j->n && (!j->desc || !j->out)) || (j->blob_sz && !j->blob) ) return FD_ED25519_ERR_ARG;
+  if( !f || !j || j->n > f->max_sigs || (j->n && (!j->desc || !j->out)) || (j->blob_sz && !j->blob) || (j->blob2_sz && !j->blob2) ) return FD_ED25519_ERR_ARG;
   j->t_push_ns = fd_feeder_now(); j->t_submit_ns = 0; j->t_done_ns = 0; j->t_pick_ns = 0;
   if( !j->n ) { fd_job_finish( j, 1 ); return 0; }
   __atomic_store_n( &j->state, 0, __ATOMIC_RELEASE );

@@ -728,16 +728,24 @@ extern "C" int fd_ed25519_gpu_kernel_cnt( void ) { return FD_ED25519_GPU_KERNEL_
    out-of-bounds one as FD_ED25519_ERR_ARG (fd_k_prep). */
 static int fd_ring_busy( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot const * sl );
 static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
-                             unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, hipStream_t * used ) {
+                             unsigned long blob_sz, void const * blob2, unsigned long blob2_sz,
+                             fd_ed25519_gpu_desc_t const * desc, hipStream_t * used ) {
+  /* the batch's bytes are blob[0, blob_sz) followed by blob2[0, blob2_sz)
+     (a second piece: an in-place batch that continues past the caller's
+     ring wrap); descriptors index the concatenation */
+  unsigned long sz0 = blob_sz;
+  blob_sz += blob2_sz;
   unsigned long doff = fd_desc_off( blob_sz );
   /* a blob in a registered region is DMA'd from where it lies (no host
      copy; descriptors go separately from the slot's pinned desc buffer);
      anything else is staged into the slot's pinned buffer with the
      descriptors packed after it (one copy) */
-  int direct = sl->h_blob != blob && blob_sz && fd_registered( g, blob, blob_sz );
+  int direct = sl->h_blob != blob && sz0 && fd_registered( g, blob, sz0 )
+            && ( !blob2_sz || fd_registered( g, blob2, blob2_sz ) );
   if( direct ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   else {
-    if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, blob_sz );
+    if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, sz0 );
+    if( blob2_sz ) memcpy( sl->h_blob + sz0, blob2, blob2_sz );
     memset( sl->h_blob + blob_sz, 0, doff - blob_sz );
     memcpy( sl->h_blob + doff, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   }
@@ -750,8 +758,10 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
   if( direct ) {
-    if( (e = hipMemcpyAsync( sl->d_blob, blob, blob_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
+    if( (e = hipMemcpyAsync( sl->d_blob, blob, sz0, hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D blob (registered)", e );
+    if( blob2_sz && (e = hipMemcpyAsync( sl->d_blob + sz0, blob2, blob2_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
+      return fd_gpu_fail( "H2D blob piece 2 (registered)", e );
     if( (e = hipMemcpyAsync( sl->d_blob + doff, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D desc", e );
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
@@ -786,9 +796,10 @@ static int fd_ring_busy( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot const * sl ) 
    leaves the slot orphaned (reclaimed by fd_free_slot once its event
    completes) instead of blocking every user of the engine lock. */
 static int fd_slot_enqueue( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, unsigned long n, void const * blob,
-                            unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc ) {
+                            unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                            void const * blob2 = NULL, unsigned long blob2_sz = 0UL ) {
   hipStream_t st = NULL;
-  int err = fd_slot_enqueue_( g, sl, n, blob, blob_sz, desc, &st );
+  int err = fd_slot_enqueue_( g, sl, n, blob, blob_sz, blob2, blob2_sz, desc, &st );
   if( err && st && fd_wait_query( fd_stream_query, (void *)st, FD_POLL_SPIN_NS, fd_timeout( g ) ) != 1 ) {
     /* the slot's done event marks the end of what was queued on st */
     if( hipEventRecord( sl->done, st ) == hipSuccess ) { sl->ticket = g->next_ticket++; sl->orphan = 1; }
@@ -822,20 +833,27 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
   return 0;
 }
 
-extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
-                                          fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
-  if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || (n && !desc) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
+extern "C" int fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                           void const * blob2, unsigned long blob2_sz,
+                                           fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || blob2_sz > g->max_blob - blob_sz || (n && !desc)
+      || (blob_sz && !blob) || (blob2_sz && !blob2) ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
   if( !sl ) return 0;                    /* ring full: poll first */
-  int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc );
+  int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc, blob2, blob2_sz );
   if( err ) return err;
   sl->staged = 0;
   sl->ticket = g->next_ticket++;
   *ticket = sl->ticket;
   return 1;
+}
+
+extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                          fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  return fd_ed25519_gpu_try_submit2( g, n, blob, blob_sz, NULL, 0UL, desc, ticket );
 }
 
 extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,

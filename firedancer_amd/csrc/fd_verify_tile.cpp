@@ -125,6 +125,12 @@ struct fd_vt_batch {
   fd_ed25519_gpu_desc_t * desc;
   unsigned long           used, nsig, ticket;
   unsigned long           first;  /* receive index of the batch's first frag */
+  /* in-place mode: a batch that continues past the wrap of the caller's
+     frag ring is two spans, [blob, blob+alen) then blob2 onwards (alen 0:
+     one span); offsets (desc, txn blob_off, used) index their
+     concatenation */
+  uint8_t const *         blob2;
+  unsigned long           alen;
   std::vector<fd_vt_txn>  txns;
   /* feeder mode */
   int                     eng;    /* engine (and feeder) the batch belongs to */
@@ -220,7 +226,10 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
     int ok = 1;
     for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( codes[ x.sig0 + k ] == FD_ED25519_SUCCESS );
     if( ok ) {
-      if( t->publish ) t->publish( t->ctx, x.tag, b->blob + x.blob_off, x.sz, x.ctl, x.tsorig, tspub );
+      if( t->publish ) {
+        uint8_t const * fp = ( b->alen && x.blob_off >= b->alen ) ? b->blob2 + (x.blob_off - b->alen) : b->blob + x.blob_off;
+        t->publish( t->ctx, x.tag, fp, x.sz, x.ctl, x.tsorig, tspub );
+      }
       t->diag[ FD_VERIFY_TILE_DIAG_PUB_CNT ]++;
       t->diag[ FD_VERIFY_TILE_DIAG_PUB_SZ  ] += x.sz;
     } else {
@@ -260,7 +269,8 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
     for(;;) {
-      int r = fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+      int r = b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, b->desc, &b->ticket )
+                      : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
       if( r == 1 ) break;
       if( r < 0 || t->inflight.empty() ) return FD_ED25519_ERR_GPU;
       t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
@@ -269,7 +279,8 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
     }
   } else if( t->multi ) {
     memset( &b->job, 0, sizeof(b->job) );
-    b->job.n = b->nsig; b->job.blob = b->blob; b->job.blob_sz = b->used; b->job.desc = b->desc; b->job.out = b->codes;
+    b->job.n = b->nsig; b->job.blob = b->blob; b->job.blob_sz = b->alen ? b->alen : b->used; b->job.desc = b->desc; b->job.out = b->codes;
+    if( b->alen ) { b->job.blob2 = b->blob2; b->job.blob2_sz = b->used - b->alen; }
     if( fd_ed25519_gpu_feeder_push( t->feeders[ b->eng ], &b->job ) ) return FD_ED25519_ERR_GPU;
     t->next = (b->eng + 1) % t->gpu_cnt;   /* the next batch goes to the next engine */
   } else {
@@ -282,14 +293,30 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
   return 0;
 }
 
-/* in-place mode: an open batch whose span can take the frag at f (frags
-   arrive at increasing addresses until the caller's ring wraps; a frag
-   below the batch's start, or past max_blob from it, closes the batch) */
+/* in-place mode: an open batch whose span can take the frag at f.  Frags
+   arrive at increasing addresses until the caller's ring wraps; at the
+   first wrap the batch continues as a second span from the lower address
+   (fd_ed25519_gpu_try_submit2: two DMA pieces), so a ring smaller than a
+   batch does not cut every batch short.  A second wrap, a frag that would
+   reach back into the first span, the signature limit or max_blob bytes
+   close the batch. */
 static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsigned long nsig, unsigned long sz ) {
   fd_vt_batch * b = t->open;
-  if( b && ( b->nsig + nsig > t->batch_sigs || f < b->blob || (unsigned long)(f - b->blob) + sz > t->max_blob ) ) {
-    int err = fd_vt_submit( t );
-    if( err ) return err;
+  if( b ) {
+    int close = b->nsig + nsig > t->batch_sigs;
+    if( !close && !b->alen ) {
+      if( f >= b->blob ) close = (unsigned long)(f - b->blob) + sz > t->max_blob;
+      else {                                    /* the ring wrapped: a second span from f */
+        close = b->used + sz > t->max_blob || f + sz > b->blob;
+        if( !close ) { b->alen = b->used; b->blob2 = f; }
+      }
+    } else if( !close ) {
+      close = f < b->blob2 || f + sz > b->blob || b->alen + (unsigned long)(f - b->blob2) + sz > t->max_blob;
+    }
+    if( close ) {
+      int err = fd_vt_submit( t );
+      if( err ) return err;
+    }
   }
   while( !t->open ) {
     fd_vt_batch * nb = NULL;
@@ -300,7 +327,7 @@ static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsig
       }
     } else if( !t->pool.empty() ) { nb = t->pool.back(); t->pool.pop_back(); }
     if( nb ) {
-      nb->blob = (uint8_t *)f; nb->used = 0; nb->nsig = 0; nb->ticket = 0;
+      nb->blob = (uint8_t *)f; nb->used = 0; nb->nsig = 0; nb->ticket = 0; nb->alen = 0; nb->blob2 = NULL;
       t->open = nb;
       break;
     }
@@ -583,7 +610,7 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
       int err = fd_vt_reserve_inplace( t, f, nsig, sz );
       if( err ) return err;
       b = t->open;
-      base = (unsigned long)(f - b->blob);
+      base = b->alen ? b->alen + (unsigned long)(f - b->blob2) : (unsigned long)(f - b->blob);
       room = base + sz > b->used ? base + sz - b->used : 0UL;   /* the span grows to the frag's end */
       FD_VT_STAMP( s3 ); FD_VT_ACC( 2, s2, s3 );
     } else {

@@ -211,6 +211,22 @@ fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t *            gpu,
                            fd_ed25519_gpu_desc_t const * desc,
                            unsigned long *               ticket );
 
+/* As fd_ed25519_gpu_try_submit for a batch whose bytes are two pieces,
+   blob[0, blob_sz) followed by blob2[0, blob2_sz) (an in-place verify tile
+   batch that continues past the wrap of the caller's frag ring): the
+   descriptors index their concatenation, blob_sz + blob2_sz <= max_blob.
+   Two pieces in registered regions are DMA'd where they lie; otherwise
+   both are staged.  blob2_sz == 0 is fd_ed25519_gpu_try_submit. */
+int
+fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t *            gpu,
+                            unsigned long                 n,
+                            void const *                  blob,
+                            unsigned long                 blob_sz,
+                            void const *                  blob2,
+                            unsigned long                 blob2_sz,
+                            fd_ed25519_gpu_desc_t const * desc,
+                            unsigned long *               ticket );
+
 int
 fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
                      unsigned long      ticket,
@@ -392,6 +408,10 @@ typedef struct fd_ed25519_gpu_job {
   int                           state;     /* written by the feeder (atomic release) */
   unsigned long                 t_push_ns, t_submit_ns, t_done_ns;
   unsigned long                 t_pick_ns;
+  /* optional second piece of the job's bytes (fd_ed25519_gpu_try_submit2:
+     the descriptors index blob || blob2); NULL / 0 for one piece */
+  void const *                  blob2;
+  unsigned long                 blob2_sz;
 } fd_ed25519_gpu_job_t;
 
 typedef struct fd_ed25519_gpu_feeder fd_ed25519_gpu_feeder_t;

@@ -109,8 +109,10 @@ fd_verify_tile_new_multi( fd_ed25519_gpu_t * const *   gpus,
    [region, region+region_sz) (e.g. the input dcache), which the tile
    registers with the engine (fd_ed25519_gpu_register) and the engine DMAs
    from directly: the frag path copies nothing.  A batch is the span of
-   its frags; frags arrive at increasing addresses, a lower one (the
-   caller's ring wrapped) closes the open batch.  A frag's bytes must stay
+   its frags; frags arrive at increasing addresses, and at the caller's
+   ring wrap the open batch continues as a second span from the lower
+   address (two DMA pieces, fd_ed25519_gpu_try_submit2); a second wrap
+   closes it.  A frag's bytes must stay
    unchanged until it is published or dropped (the reference's flow
    control: credits return after the frag is consumed).  NULL if the
    region cannot be registered.  Same semantics and counters as

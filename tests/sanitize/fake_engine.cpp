@@ -14,6 +14,7 @@
    (fake_engine_wedge): batches submitted while it is on never complete. */
 #include <stdlib.h>
 #include <string.h>
+#include <vector>
 #include <mutex>
 #include "fd_ed25519_gpu.h"
 #include "fd_ed25519_gpu_desc.h"
@@ -99,6 +100,18 @@ extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n,
   sl->ticket = g->next++;
   *ticket = sl->ticket;
   return 1;
+}
+/* two pieces: staged into one buffer, then the one-piece path (the fake
+   slot's blob is max_blob bytes) */
+extern "C" int fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                           void const * blob2, unsigned long blob2_sz,
+                                           fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  if( !blob2_sz ) return fd_ed25519_gpu_try_submit( g, n, blob, blob_sz, desc, ticket );
+  if( !g || !blob2 || blob_sz > g->max_blob || blob2_sz > g->max_blob - blob_sz ) return FD_ED25519_ERR_ARG;
+  std::vector<uint8_t> cat( blob_sz + blob2_sz );
+  if( blob_sz ) memcpy( cat.data(), blob, blob_sz );
+  memcpy( cat.data() + blob_sz, blob2, blob2_sz );
+  return fd_ed25519_gpu_try_submit( g, n, cat.data(), cat.size(), desc, ticket );
 }
 extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
                                       fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {

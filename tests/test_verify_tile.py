@@ -192,9 +192,11 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob, engines):
     """The in-place mode (fd_verify_tile_new_inplace): frags live in one
     registered region (the input dcache's stand-in) and each batch is DMA'd
     from its span there, no copy.  The stream is fed in two passes over two
-    halves placed in reverse address order (the second half first), so a
-    batch also closes when the caller's ring "wraps" to a lower address, and
-    a small max_blob closes batches on span size.  Publishes and counters
+    halves placed in reverse address order (the second half first), so the
+    caller's ring "wraps" to a lower address once: the batch open at the
+    wrap continues as a second span (fd_ed25519_gpu_try_submit2, two DMA
+    pieces) and the batches equal those of the same stream laid out
+    contiguously; a small max_blob closes batches on span size.  Publishes and counters
     equal the reference's per-frag semantics, in arrival order.  With
     engines > 1 the tile runs the multi-engine feeder mode in place
     (fd_verify_tile_new_multi_inplace: the one region registered with
@@ -236,6 +238,21 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob, engines):
         tile.rx_burst(other, np.zeros(1, np.uint64), np.array([len(other)], np.uint32))
         assert tile.diag()["BAD_CNT"] == exp["BAD_CNT"] + 1
         tile.close()
+        # the wrap no longer closes a batch: the batch open at the wrap
+        # continues as a second span (two DMA pieces), so the same stream
+        # laid out contiguously gives the same batches
+        lay2 = first + second
+        sz2 = np.array([len(f) for f in lay2], np.uint32)
+        off2 = np.concatenate([[0], np.cumsum(sz2)[:-1]]).astype(np.uint64)
+        region2 = np.frombuffer(b"".join(lay2) + b"\0" * 64, np.uint8).copy()
+        tile2 = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region2)
+        for a in range(0, len(lay2), 97):
+            tile2.rx_burst(region2, off2[a:a + 97], sz2[a:a + 97], ctl=np.arange(a, min(a + 97, len(lay2)), dtype=np.uint64))
+            tile2.service()
+        tile2.service(flush=True)
+        assert [(s2, f2) for s2, f2, _, _ in tile2.published] == exp_pub
+        assert tile2.diag()["BATCH_CNT"] == d["BATCH_CNT"], (tile2.diag()["BATCH_CNT"], d["BATCH_CNT"])
+        tile2.close()
     finally:
         for e in es:
             e.close()

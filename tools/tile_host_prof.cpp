@@ -74,6 +74,12 @@ extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n,
   }
   return 0;
 }
+extern "C" int fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t * g, unsigned long n, void const * blob, unsigned long blob_sz,
+                                           void const * blob2, unsigned long blob2_sz,
+                                           fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
+  (void)blob2; (void)blob2_sz;
+  return fd_ed25519_gpu_try_submit( g, n, blob, blob_sz, desc, ticket );
+}
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
   (void)block;
   for( int s=0; s<IDEPTH; s++ ) if( g->ticket[s] == ticket ) {
