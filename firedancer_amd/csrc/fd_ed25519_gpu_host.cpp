@@ -144,6 +144,7 @@ struct fd_ed25519_gpu {
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long oct_max;  /* and batches <= this the eight-lane DSM */
   unsigned long out_direct_max;  /* ring batches <= this get their codes written to pinned memory by the DSM */
+  unsigned long blob_cap;        /* bytes of a slot's blob buffers (padded blob + descriptors) */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
   int           group_always; /* experiments (FD_ED25519_GPU_GROUP_ALWAYS=1): a lone ring batch also runs on its CU group */
@@ -200,6 +201,22 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
   w->ops      = (uint8_t *)p; p += (unsigned long)FD_OPS_MAX * N;
 }
 
+/* First use of a stream, not engine creation, pays for its queues: the
+   first H2D copy, kernel and D2H copy on a fresh stream (a CU-masked one
+   most of all) cost milliseconds -- the 8.7-9.1 ms maximum of the
+   16-thread per-signature runs, when a third group-commit leader first
+   used its slot (profiles/r04_in_direct_ab.jsonl).  Engine creation
+   therefore sends copies of every size class each way and one blit
+   kernel down every stream a batch can take. */
+static hipError_t fd_stream_warm( hipStream_t st, fd_ed25519_gpu_slot * sl, unsigned long cap ) {
+  hipError_t e;
+  for( unsigned long sz=64UL; sz<=cap && sz<=(4UL<<20); sz<<=3 )
+    if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, sz, hipMemcpyHostToDevice, st )) != hipSuccess ) return e;
+  if( (e = hipMemsetAsync( sl->d_out, 0, 64, st )) != hipSuccess ) return e;
+  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, 64, hipMemcpyDeviceToHost, st )) != hipSuccess ) return e;
+  return hipStreamSynchronize( st );
+}
+
 /* (Re)create the slots' CU-masked streams: slot s runs on group s mod
    groups, a contiguous range of logical CUs (physically spread over all
    8 XCDs, disjoint from the other groups).
@@ -222,7 +239,8 @@ static void fd_cu_groups_make( fd_ed25519_gpu_t * g, int groups ) {
        interleaved mask (CU c in group c mod groups) used before reached
        all 256 physical CUs from every group -- no isolation at all */
     for( int c=0; c<ncu; c++ ) if( c / (ncu / groups) == s % groups ) mask[c >> 5] |= 1u << (c & 31);
-    if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess ) {
+    if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess
+        || fd_stream_warm( g->slot[s].mstream, &g->slot[s], g->blob_cap ) != hipSuccess ) {
       (void)hipGetLastError();
       for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
       g->mask_max = 0UL; g->groups = 1;
@@ -266,6 +284,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
      copy (a second small copy costs ~17 us of a ~0.75 ms 4096-signature
      round trip: its own transfer plus the copy-to-copy gap) */
   unsigned long blob_cap = fd_desc_off( max_blob ) + max_sigs * sizeof(fd_ed25519_gpu_desc_t);
+  g->blob_cap = blob_cap;
   HIPCHK( hipSetDevice( device ) );
   HIPCHK( fd_ed25519_gpu_upload_tables() );
   for( int s=0; s<g->depth; s++ ) {
@@ -285,6 +304,8 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipStreamCreateWithFlags( &sl->stream, hipStreamNonBlocking ) );
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
+    memset( sl->h_blob, 0, blob_cap < (4UL<<20) ? blob_cap : (4UL<<20) );   /* the warm copies land zeros (d_blob stays zeroed) */
+    HIPCHK( fd_stream_warm( sl->stream, sl, blob_cap ) );
   }
   /* CU groups for small ring batches.  A 4,096-signature batch on the
      latency schedule is lone waves (256 quad-DSM waves, 192 front-end

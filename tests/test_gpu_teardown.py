@@ -1,0 +1,70 @@
+"""Process teardown with engines still alive (round-3 verdict, weak item 8:
+a per-signature run crashed in __cxa_finalize under rocprofv3 when the
+process-default engine was left to the HIP runtime's own teardown; the
+fix releases it from an atexit handler, fd_ed25519_gpu_host.cpp
+fd_default_engine_fini).  Each case runs in a child process that exits
+without closing what it created; the child must exit 0 with its codes
+right, and nothing on stderr may name a fault."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+PRELUDE = f"""
+import sys
+sys.path.insert(0, {ROOT!r})
+import numpy as np
+import firedancer_amd as fa
+from firedancer_amd import corpus
+b = corpus.adversarial(64, 100, seed=77, invalid_frac=0.3)
+"""
+
+CASES = {
+    # the process-default engine (fd_ed25519_verify) left for atexit
+    "default_engine": """
+e = fa.Engine(0, 1 << 12, 1 << 22)
+exp = e.verify_packed(b.blob, b.desc)
+e.close()
+for i in range(0, 64, 7):
+    assert fa.verify(b.msg(i), b.sig(i), b.pub(i)) == exp[i]
+r, out = fa.verify_batch([b.msg(i) for i in range(64)], [b.sig(i) for i in range(64)], [b.pub(i) for i in range(64)])
+assert (out == exp).all()
+print("ok", flush=True)
+""",
+    # explicit engine + feeder never closed (interpreter shutdown order)
+    "unclosed_engine_and_feeder": """
+e = fa.Engine(0, 1 << 12, 1 << 22)
+exp = e.verify_packed(b.blob, b.desc)
+f = fa.Feeder(e)
+out = np.full(64, 99, np.int32)
+j = f.push(b.blob, b.desc, out)
+f.wait(j)
+assert (out == exp).all()
+fa._keep = (e, f)        # still referenced at exit
+print("ok", flush=True)
+""",
+    # a batch still on the ring when the process exits
+    "exit_with_batch_in_flight": """
+e = fa.Engine(0, 1 << 12, 1 << 22)
+big = corpus.solana_txns(4096, seed=78)
+t = e.submit(big.blob, big.desc)
+fa._keep = e
+print("ok", flush=True)
+""",
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_exit_with_live_engines(case):
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, "-c", PRELUDE + CASES[case]], capture_output=True, text=True,
+                       timeout=180, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert r.stdout.strip().endswith("ok"), r.stdout[-2000:]
+    for bad in ("Segmentation fault", "core dumped", "Aborted", "HSA_STATUS_ERROR", "Memory access fault"):
+        assert bad not in r.stderr, r.stderr[-4000:]
