@@ -208,10 +208,15 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
    used its slot (profiles/r04_in_direct_ab.jsonl).  Engine creation
    therefore sends copies of every size class each way and one blit
    kernel down every stream a batch can take. */
+#define FD_WARM_MAX (16UL<<20)
 static hipError_t fd_stream_warm( hipStream_t st, fd_ed25519_gpu_slot * sl, unsigned long cap ) {
   hipError_t e;
-  for( unsigned long sz=64UL; sz<=cap && sz<=(4UL<<20); sz<<=3 )
+  unsigned long top = cap < FD_WARM_MAX ? cap : FD_WARM_MAX;
+  for( unsigned long sz=64UL; ; sz<<=3 ) {
+    if( sz > top ) sz = top;
     if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, sz, hipMemcpyHostToDevice, st )) != hipSuccess ) return e;
+    if( sz == top ) break;
+  }
   if( (e = hipMemsetAsync( sl->d_out, 0, 64, st )) != hipSuccess ) return e;
   if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, 64, hipMemcpyDeviceToHost, st )) != hipSuccess ) return e;
   return hipStreamSynchronize( st );
@@ -304,7 +309,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipStreamCreateWithFlags( &sl->stream, hipStreamNonBlocking ) );
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
-    memset( sl->h_blob, 0, blob_cap < (4UL<<20) ? blob_cap : (4UL<<20) );   /* the warm copies land zeros (d_blob stays zeroed) */
+    memset( sl->h_blob, 0, blob_cap < FD_WARM_MAX ? blob_cap : FD_WARM_MAX );   /* the warm copies land zeros (d_blob stays zeroed) */
     HIPCHK( fd_stream_warm( sl->stream, sl, blob_cap ) );
   }
   /* CU groups for small ring batches.  A 4,096-signature batch on the
