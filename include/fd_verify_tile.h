@@ -237,7 +237,7 @@ typedef struct {
   /* set by the caller (the reference reads these from its pod) */
   int                        device;
   unsigned long              max_sigs, max_blob;    /* engine batch capacity */
-  int                        depth;                 /* ring slots, 0 -> 3 */
+  int                        depth;                 /* ring slots; 0 -> 8 if max_sigs <= 32768, else 3 */
   fd_verify_tile_cfg_t       cfg;
   fd_verify_tile_cnc_t *     cnc;
   fd_verify_tile_in_fn       in;       void * in_ctx;
