@@ -41,6 +41,26 @@ int main( int argc, char ** argv ) {
   printf( "]}\n" );
   if( r ) return 10 + r;
 
+  /* in place: the same frags written into a ring region (rings smaller
+     and larger than a batch, spans closed by max_blob), the publish stream
+     and every counter but the batch count equal to pass 1's */
+  {
+    unsigned long rings[3] = { 24UL << 10, 96UL << 10, 4UL << 20 };
+    unsigned long bsigs[3] = { 1024, 128, 4096 };
+    unsigned long mblob[3] = { 8UL << 20, 64UL << 10, 8UL << 20 };
+    for( int k=0; k<3; k++ ) {
+      tc_state si; unsigned long di[ FD_VERIFY_TILE_DIAG_CNT ];
+      int ri = tc_run_inplace( fr.data(), sz.data(), n, bsigs[k], mblob[k], 2 + k, rings[k], &si, di );
+      int same = si.pub_cnt == st.pub_cnt && si.hash == st.hash;
+      for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ )
+        if( c != FD_VERIFY_TILE_DIAG_BATCH_CNT ) same &= di[c] == diag[c];
+      printf( "{\"pass\": \"inplace%d\", \"rc\": %d, \"ring\": %lu, \"pub_cnt\": %lu, \"batches\": %lu, \"same\": %d}\n",
+              k, ri, rings[k], si.pub_cnt, di[FD_VERIFY_TILE_DIAG_BATCH_CNT], same );
+      if( ri ) return 40 + ri;
+      if( !same ) return 50 + k;
+    }
+  }
+
   /* corrupted streams */
   unsigned long seed = 0x243f6a8885a308d3UL;
   unsigned long bsz[4] = { 16, 128, 1024, 4096 };
@@ -61,6 +81,12 @@ int main( int argc, char ** argv ) {
       if( u == 6 ) { unsigned char * q = (unsigned char *)malloc( x.size() ? x.size() : 1 ); memcpy( q, x.data(), x.size() ); cf.push_back( q ); cs.push_back( x.size() ); }
     }
     r = tc_run( cf.data(), cs.data(), cf.size(), bsz[round % 4], 2UL << 20, 1 + round % 4, &st, diag );
+    if( !r ) {   /* and in place through a 32 KiB ring: same publishes */
+      tc_state si; unsigned long di[ FD_VERIFY_TILE_DIAG_CNT ];
+      int ri = tc_run_inplace( cf.data(), cs.data(), cf.size(), bsz[round % 4], 2UL << 20, 1 + round % 4, 32UL << 10, &si, di );
+      if( ri ) return 60 + ri;
+      if( si.hash != st.hash || si.pub_cnt != st.pub_cnt ) return 70;
+    }
     printf( "{\"pass\": %d, \"rc\": %d, \"frags\": %lu, \"pub_cnt\": %lu, \"bad\": %lu, \"sv\": %lu}\n", round + 2, r,
             (unsigned long)cf.size(), st.pub_cnt, diag[FD_VERIFY_TILE_DIAG_BAD_CNT], diag[FD_VERIFY_TILE_DIAG_SV_FILT_CNT] );
     for( unsigned char * p : cf ) free( p );
