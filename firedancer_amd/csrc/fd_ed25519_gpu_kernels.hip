@@ -984,6 +984,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
+  uint64_t const okw = fd_op_kind_word( q );
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
@@ -992,10 +993,10 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
        any other row's bytes only steer lanes whose result is discarded
        (code != FD_ST_PENDING), with table indices bounded by the masks */
     int op = (int)L.ops[ls][t];
-    uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
-    uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
+    uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
+    uint32_t add = fd_ok_mask( kd, FD_OK_QS );
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
-    uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
+    uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
     int32_t E[10];
     {
       int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
@@ -1010,8 +1011,8 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     /* f: q0 X+Y, q1 Z, q2 Y (A: Y-X), q3 X (A: T); g: D f (q1 2Z), A E */
     fe u, w;
     fd_fe_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fe_qperm<FD_QP(2,2,2,2)>( w, C );
-    uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
-    uint32_t gs = (q==1u && !add) ? 1u : 0u;
+    uint32_t mW = fd_ok_mask( kd, FD_OK_MW ), mT = fd_ok_mask( kd, FD_OK_MT );
+    uint32_t gs = fd_ok_bits( kd, FD_OK_GS, 1 );
     /* u + fd_qterm( w, mW, mq2 ) as u + ((w & mW) ^ mq2) + (mq2 & 1): one
        v_bitop3 and one v_add3 per limb (-s == s & 1 for a mask s; LLVM
        otherwise selects between w & mW and its negation) */
@@ -1029,12 +1030,10 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
          q1 D: R+S        A: P+R
          q2 D: R-S        A: 2Q-S (positive digit: 2Q+S)
          q3 D: Q-R+S      A: 2Q+S (positive digit: 2Q-S) */
-    uint32_t pos = add & ~neg;
-    uint32_t mP = mq0 | (mq1 & add);
-    uint32_t mQ = mq3 | (mq2 & add), qs = add ? 1u : 0u;
-    uint32_t mR = mq0 | mq1 | ~add, sR = mq0 | (mq3 & ~add);
-    uint32_t mS = ~((mq0 | mq1) & add), sS = (mq0 & ~add) | (mq2 & ~pos) | (mq3 & pos);
-    uint32_t cadd = (sR & 1u) + (sS & 1u);
+    uint32_t mP = fd_ok_mask( kd, FD_OK_MP ), mQ = fd_ok_mask( kd, FD_OK_MQ ), qs = fd_ok_bits( kd, FD_OK_QS, 1 );
+    uint32_t mR = fd_ok_mask( kd, FD_OK_MR ), sR = fd_ok_mask( kd, FD_OK_SR );
+    uint32_t mS = fd_ok_mask( kd, FD_OK_MS ), sS = fd_ok_mask( kd, FD_OK_SS );
+    uint32_t cadd = fd_ok_bits( kd, FD_OK_CADD, 2 );
 #if FD_QUAD_DPP_AND
     /* each broadcast masked by a v_and_b32 with the quad move folded in
        (VOP2 DPP); the barriers keep LLVM from fusing and + xor into a
@@ -1426,6 +1425,7 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   __syncthreads();
 
   /* main loop: the quad's step on half field elements */
+  uint64_t const okw = fd_op_kind_word( q );
   fh s;
 #pragma unroll
   for( int k=0; k<5; k++ ) s.v[k] = 0;
@@ -1434,9 +1434,9 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   unsigned long long os_c0 = __builtin_amdgcn_s_memtime(), os_r0 = __builtin_amdgcn_s_memrealtime();
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
     int op = (int)L.ops[ls][t];
-    uint32_t add = (op & FD_OP_ADD) ? ~0u : 0u;
-    uint32_t neg = ((op >> 5) & 1) ? ~0u : 0u;
-    uint32_t idx = q==0u ? (neg ? 1u : 2u) : q==1u ? 0u : q==2u ? (neg ? 2u : 1u) : 3u;
+    uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
+    uint32_t add = fd_ok_mask( kd, FD_OK_QS );
+    uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
     int32_t E[5];
     {
       int32_t const * ent = ((op & 0x40) ? L.tab[FD_OSIGS] : L.tab[ls]) + (op & 7)*FD_OTAB_ENTRY + idx*FD_OTAB_LANE + 8u*h;
@@ -1450,8 +1450,8 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
 
     fh u, w;
     fd_fh_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fh_qperm<FD_QP(2,2,2,2)>( w, C );
-    uint32_t mW = mq0 | (mq2 & add), mT = mq3 & add;
-    uint32_t gs = (q==1u && !add) ? 1u : 0u;
+    uint32_t mW = fd_ok_mask( kd, FD_OK_MW ), mT = fd_ok_mask( kd, FD_OK_MT );
+    uint32_t gs = fd_ok_bits( kd, FD_OK_GS, 1 );
     uint32_t const s2b = (uint32_t)fd_opaque( (int32_t)(mq2 & 1u) );
 #pragma unroll
     for( int k=0; k<5; k++ ) {
@@ -1461,12 +1461,10 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
     }
     fh hq; fd_o_mul( hq, fo, go, oc );
 
-    uint32_t pos = add & ~neg;
-    uint32_t mP = mq0 | (mq1 & add);
-    uint32_t mQ = mq3 | (mq2 & add), qs = add ? 1u : 0u;
-    uint32_t mR = mq0 | mq1 | ~add, sR = mq0 | (mq3 & ~add);
-    uint32_t mS = ~((mq0 | mq1) & add), sS = (mq0 & ~add) | (mq2 & ~pos) | (mq3 & pos);
-    uint32_t cadd = (sR & 1u) + (sS & 1u);
+    uint32_t mP = fd_ok_mask( kd, FD_OK_MP ), mQ = fd_ok_mask( kd, FD_OK_MQ ), qs = fd_ok_bits( kd, FD_OK_QS, 1 );
+    uint32_t mR = fd_ok_mask( kd, FD_OK_MR ), sR = fd_ok_mask( kd, FD_OK_SR );
+    uint32_t mS = fd_ok_mask( kd, FD_OK_MS ), sS = fd_ok_mask( kd, FD_OK_SS );
+    uint32_t cadd = fd_ok_bits( kd, FD_OK_CADD, 2 );
     uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
     uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
 #pragma unroll
