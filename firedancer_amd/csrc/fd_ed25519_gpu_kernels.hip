@@ -932,7 +932,8 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      LDS as 16-byte pieces from the wave's first op on: at most 8
      independent loads per lane (a byte per lane per load, as before, was a
      ~100-deep chain of dependent round trips in front of the first step) */
-  int t0 = fd_wave_min( start );
+  /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
+  int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
   {
     int const c0 = t0 >> 4;
     for( int c=(int)lane; c<FD_QSIGS*(FD_OPS_MAX/16); c+=64 ) {
@@ -985,6 +986,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
   uint64_t const okw = fd_op_kind_word( q );
+  uint32_t const tab_bi = (uint32_t)(L.tab[FD_QSIGS] - tab_s);   /* int32s from this signature's Ai to Bi */
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
@@ -999,7 +1001,9 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
     int32_t E[10];
     {
-      int32_t const * ent = ((op & 0x40) ? L.tab[FD_QSIGS] : tab_s) + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
+      /* Bi (op bit 6) or this signature's Ai: the row offset by arithmetic,
+         not a compare and select (a VALU-written SGPR mask costs wait states) */
+      int32_t const * ent = tab_s + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
       int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
     }
@@ -1373,7 +1377,8 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
     rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
   }
 
-  int t0 = fd_wave_min( start );
+  /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
+  int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
   {
     int const c0 = t0 >> 4;
     for( int c=(int)lane; c<FD_OSIGS*(FD_OPS_MAX/16); c+=64 ) {
@@ -1426,6 +1431,7 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
 
   /* main loop: the quad's step on half field elements */
   uint64_t const okw = fd_op_kind_word( q );
+  uint32_t const tab_bi = (uint32_t)(L.tab[FD_OSIGS] - L.tab[ls]);   /* int32s from this signature's Ai to Bi */
   fh s;
 #pragma unroll
   for( int k=0; k<5; k++ ) s.v[k] = 0;
@@ -1439,7 +1445,8 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
     uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
     int32_t E[5];
     {
-      int32_t const * ent = ((op & 0x40) ? L.tab[FD_OSIGS] : L.tab[ls]) + (op & 7)*FD_OTAB_ENTRY + idx*FD_OTAB_LANE + 8u*h;
+      /* Bi (op bit 6) or this signature's Ai, as the quad */
+      int32_t const * ent = L.tab[ls] + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_OTAB_ENTRY + idx*FD_OTAB_LANE + 8u*h;
       int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1];
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x;
     }
