@@ -199,6 +199,7 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
   w->pstat    = (int32_t *)p; p +=    8UL * N;
   w->op_start = (int32_t *)p; p +=    4UL * N;
   w->ops      = (uint8_t *)p; p += (unsigned long)FD_OPS_MAX * N;
+  w->sdig     = (uint32_t *)p;                   /* FD_SDIG_BYTES, 16-byte aligned (every array above is) */
 }
 
 /* First use of a stream, not engine creation, pays for its queues: the
@@ -304,8 +305,9 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipMemset( sl->d_blob, 0, blob_cap ) );
     HIPCHK( hipMalloc( (void **)&sl->d_desc, max_sigs * sizeof(fd_ed25519_gpu_desc_t) ) );
     HIPCHK( hipMalloc( (void **)&sl->d_out,  max_sigs * sizeof(int32_t) ) );
-    HIPCHK( hipMalloc( &sl->d_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
+    HIPCHK( hipMalloc( &sl->d_work_base, FD_ED25519_GPU_WORK_PER_SIG * max_sigs + FD_SDIG_BYTES ) );
     fd_work_carve( &sl->work, sl->d_work_base, max_sigs );
+    HIPCHK( hipMemset( sl->work.sdig, 0, FD_SDIG_BYTES ) );   /* launch tags start at 1 */
     HIPCHK( hipStreamCreateWithFlags( &sl->stream, hipStreamNonBlocking ) );
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
@@ -346,8 +348,9 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipStreamCreateWithPriority( &g->dev_sb, hipStreamNonBlocking, hi ) );
   }
   for( int b=0; b<2; b++ ) {
-    HIPCHK( hipMalloc( &g->d_dev_work_base[b], FD_ED25519_GPU_WORK_PER_SIG * max_sigs ) );
+    HIPCHK( hipMalloc( &g->d_dev_work_base[b], FD_ED25519_GPU_WORK_PER_SIG * max_sigs + FD_SDIG_BYTES ) );
     fd_work_carve( &g->dev_work[b], g->d_dev_work_base[b], max_sigs );
+    HIPCHK( hipMemset( g->dev_work[b].sdig, 0, FD_SDIG_BYTES ) );
     HIPCHK( hipEventCreateWithFlags( &g->dev_in[b],    hipEventDisableTiming ) );
     HIPCHK( hipEventCreateWithFlags( &g->dev_front[b], hipEventDisableTiming ) );
     HIPCHK( hipEventCreateWithFlags( &g->dev_back[b],  hipEventDisableTiming ) );

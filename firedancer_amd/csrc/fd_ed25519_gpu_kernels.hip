@@ -130,6 +130,7 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 }
 
 #include "fd_ed25519_gpu_wnaf.h"
+#include <atomic>
 
 static __device__ __forceinline__ void
 fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
@@ -229,7 +230,7 @@ static __device__ __forceinline__ void
 fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
                fd_ed25519_gpu_desc_t const * __restrict__ desc,
                int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-               fd_lds_u8 * stage, fd_sha2_lds_ring * ring ) {
+               fd_lds_u8 * stage, fd_sha2_lds_ring * ring, uint32_t * __restrict__ sdig, uint32_t tag ) {
   uint32_t const wv = threadIdx.x >> 6;
   bool live = i < n;
   fd_ed25519_gpu_desc_t d = live ? desc[i] : fd_ed25519_gpu_desc_t{ 0, 0, 0, 0 };
@@ -311,7 +312,29 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
      exited) */
   typedef __attribute__((address_space(3))) uint16_t lds_u16;
   static_assert( sizeof(fd_sha2_ring) >= FD_RECODE2_SLOTS*64*sizeof(uint16_t), "recoder slots fit the chunk ring" );
-  op_start[i] = fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, (lds_u16 *)ring + (threadIdx.x & 63u), 64u );
+  lds_u16 * const slots = (lds_u16 *)ring + (threadIdx.x & 63u);
+  /* a small batch's S digits were recoded ahead by an idle front-end wave
+     (fd_sdig_body): published with this launch's tag, they are copied into
+     the slots and only k's pass runs here; else both passes */
+  int ns = -1;
+  if( sdig && n <= FD_SDIG_SIGS ) {
+    uint32_t * const e = sdig + i*FD_SDIG_DW;
+    if( __hip_atomic_load( e + 33, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT ) == tag ) {
+      uint4 d[8];
+#pragma unroll
+      for( int c=0; c<8; c++ ) d[c] = ((uint4 const *)e)[c];
+      ns = (int)e[32];
+#pragma unroll
+      for( int c=0; c<8; c++ ) {
+        uint32_t const x[4] = { d[c].x, d[c].y, d[c].z, d[c].w };
+#pragma unroll
+        for( int h=0; h<8; h++ )
+          if( 8*c + h < ns ) slots[(uint32_t)(8*c + h)*64u] = (uint16_t)(x[h >> 1] >> ((h & 1) ? 16 : 0));
+      }
+    }
+  }
+  op_start[i] = ns >= 0 ? fd_recode2_k( kw, ops + i*FD_OPS_MAX, 1, slots, 64u, ns )
+                        : fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, slots, 64u );
 #ifdef FD_FRONT_STAMPS
   {
     unsigned long long ts3;
@@ -509,6 +532,29 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
 #if FD_PREP2 && FD_FRONT_WAVES != 2
 #error "fd_prep2_body runs on exactly two waves per block (rounds + schedule)"
 #endif
+/* The S pass of the recoder (fd_recode2_s) run ahead for batches of at
+   most FD_SDIG_SIGS signatures, on the first decomp block's second wave,
+   which holds no points then (2n <= 64): the digits go to the slot's
+   scratch and the launch tag publishes them; the prep round wave, which
+   reaches its recoder only after SHA-512 (tens of us later), takes them if
+   the tag matches and otherwise recodes S itself -- nothing waits on this
+   wave.  Signatures that fail the S check or a descriptor bound are
+   skipped (prep never recodes them). */
+static __device__ __forceinline__ void
+fd_sdig_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+              fd_ed25519_gpu_desc_t const * __restrict__ desc, uint32_t * __restrict__ sdig, uint32_t tag ) {
+  if( i >= n ) return;
+  fd_ed25519_gpu_desc_t d = desc[i];
+  if( !fd_desc_in( d, blob_sz ) ) return;
+  uint32_t sw[8]; fd_ld32( sw, blob + d.sig_off + 32u );
+  uint32_t const s31 = sw[7] >> 24;
+  if( s31 >= 0x10u ) return;     /* at or above 2^252: rejected or an early accept, or the rare S < L just above it */
+  uint32_t * const e = sdig + i*FD_SDIG_DW;
+  int ns = fd_recode2_s( sw, (uint16_t *)e, 1u );
+  e[32] = (uint32_t)ns;
+  __hip_atomic_store( e + 33, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT );
+}
+
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only (tools/front_stamps.py): histograms of the
    front end's per-wave execution time (s_memrealtime, 100 MHz ticks, 2 us
@@ -522,7 +568,8 @@ extern "C" hipError_t fd_ed25519_gpu_front_hist( void * host, int clear ) {
 extern "C" __global__ void __launch_bounds__(64*FD_FRONT_WAVES)
 fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
-            int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep ) {
+            int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep,
+            uint32_t * __restrict__ sdig, uint32_t tag ) {
 #if FD_PREP2 && FD_PREP2_DIRECT
   __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
   fd_lds_u8 * const sha_stage = NULL;
@@ -541,11 +588,16 @@ fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_
   if( blockIdx.x < nb_prep ) {
 #if FD_PREP2
     fd_prep2_body( (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u), n, blob, blob_sz, desc, status, ops, op_start, strict,
-                   (fd_lds_u8 *)sha_stage, (fd_sha2_lds_ring *)&sha_ring );
+                   (fd_lds_u8 *)sha_stage, (fd_sha2_lds_ring *)&sha_ring, strict ? NULL : sdig, tag );
 #else
     fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, NULL, 1 );
 #endif
-  } else
+  }
+#if FD_PREP2
+  else if( sdig && !strict && n <= FD_SDIG_SIGS && blockIdx.x == nb_prep && threadIdx.x >= 64u )
+    fd_sdig_body( (uint64_t)threadIdx.x - 64u, n, blob, blob_sz, desc, sdig, tag );   /* this wave holds no points: 2n <= 64 */
+#endif
+  else
     fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
 #ifdef FD_FRONT_STAMPS
   __builtin_amdgcn_wave_barrier();
@@ -2033,8 +2085,13 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
     unsigned const bt = 64u*FD_FRONT_WAVES;
     unsigned const ps = FD_PREP2 ? 64u : bt;   /* signatures per prep block */
     unsigned const fp = (unsigned)((n + ps - 1) / ps), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
+    /* the tag that publishes this launch's S digits (fd_sdig_body): never 0
+       (the scratch starts zeroed), never an earlier launch's on this buffer */
+    static std::atomic<uint32_t> fd_front_tag{ 0u };
+    uint32_t tag = fd_front_tag.fetch_add( 1u ) + 1u;
+    if( !tag ) tag = fd_front_tag.fetch_add( 1u ) + 1u;
     hipLaunchKernelGGL( fd_k_front, dim3(fp + fd), dim3(bt), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start,
-                        w->pstat, w->pts, portable, strict, fp );
+                        w->pstat, w->pts, portable, strict, fp, w->sdig, tag );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
     hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,

@@ -16,7 +16,9 @@
      tab      int32 [N][384]     per-signature Ai table, AoS [entry 8][lane 4][12]
                                  (10 limbs + 2 pad: 48-byte lanes, 16-byte aligned)
      fin      int32 [N][40]      the pooled DSM's final p1p1 states, one 160-byte row
-                                 per signature (fd_k_dsm_pool -> fd_k_dsm_final) */
+                                 per signature (fd_k_dsm_pool -> fd_k_dsm_final)
+     sdig     u32 [32][36]       S's digits recoded ahead (batches <= 32, fd_k_front);
+                                 a fixed FD_SDIG_BYTES after the per-signature arrays */
 typedef struct fd_ed25519_gpu_work {
   int32_t * status;
   uint8_t * ops;
@@ -25,7 +27,15 @@ typedef struct fd_ed25519_gpu_work {
   int32_t * pts;
   int32_t * tab;
   int32_t * fin;
+  uint32_t * sdig;    /* [FD_SDIG_SIGS][FD_SDIG_DW]: S's digits recoded ahead for small batches */
 } fd_ed25519_gpu_work_t;
+
+/* S-digit scratch of the latency front end (fd_k_front, batches of at most
+   FD_SDIG_SIGS signatures): per signature 64 u16 digit slots (32 dwords),
+   the digit count and the launch tag that publishes them, padded to 16 B */
+#define FD_SDIG_SIGS  32UL
+#define FD_SDIG_DW    36UL
+#define FD_SDIG_BYTES (FD_SDIG_SIGS*FD_SDIG_DW*4UL)
 
 /* bytes of HBM working set per signature of capacity */
 /* number of kernels in one launch (timed API) */

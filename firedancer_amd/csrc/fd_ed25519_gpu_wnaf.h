@@ -201,11 +201,12 @@ FD_DEV int fd_recode( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t 
    its registers.  A pending S is below L < 2^253, whose width-5 digits are
    at least 5 bits apart: at most 51 of them.  The front end parks them in
    its SHA-512 chunk ring, which is free once the round wave has consumed
-   the last chunk (8 KiB = 64 slots x 64 lanes). */
+   the last chunk (8 KiB = 64 slots x 64 lanes).  Small batches run the S
+   pass ahead, on an idle wave of the front end (fd_sdig_body). */
 #define FD_RECODE2_SLOTS 64
-template<typename BUF>   /* uint16_t * (host), or an LDS (address space 3) pointer */
-FD_DEV int fd_recode2( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t * ops, uint64_t stride,
-                       BUF buf, uint32_t bstride ) {
+/* pass 1: S's digits into buf (returns their count) */
+template<typename BUF>   /* uint16_t * (host or global), or an LDS (address space 3) pointer */
+FD_DEV int fd_recode2_s( uint32_t const (&sw)[8], BUF buf, uint32_t bstride ) {
   fd_wn v;
   fd_wn_init( v, sw );
   int ns = 0;
@@ -216,6 +217,12 @@ FD_DEV int fd_recode2( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t
     buf[(uint32_t)ns*bstride] = (uint16_t)(((uint32_t)b << 8) | fd_op_enc( 1, dg ));
     ns++;
   }
+  return ns;
+}
+/* pass 2: k's digits merged with the ns S digits in buf; returns op_start */
+template<typename BUF>
+FD_DEV int fd_recode2_k( uint32_t const (&kw)[8], uint8_t * ops, uint64_t stride, BUF buf, uint32_t bstride, int ns ) {
+  fd_wn v;
   int cnt = 0, si = 0, nk = 0;
   uint32_t nx = ns ? (uint32_t)buf[0] : 0x10000u;     /* S's next digit; 0x10000: none left */
   fd_wn_init( v, kw );
@@ -237,6 +244,12 @@ FD_DEV int fd_recode2( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t
     nx = si < ns ? (uint32_t)buf[(uint32_t)si*bstride] : 0x10000u;
   }
   return FD_OPS_MAX - 256 - cnt;
+}
+template<typename BUF>
+FD_DEV int fd_recode2( uint32_t const (&sw)[8], uint32_t const (&kw)[8], uint8_t * ops, uint64_t stride,
+                       BUF buf, uint32_t bstride ) {
+  int ns = fd_recode2_s( sw, buf, bstride );
+  return fd_recode2_k( kw, ops, stride, buf, bstride, ns );
 }
 
 #endif /* FD_ED25519_GPU_WNAF_H */
