@@ -210,16 +210,17 @@ static void fd_work_carve( fd_ed25519_gpu_work_t * w, void * base, unsigned long
    therefore sends copies of every size class each way and one blit
    kernel down every stream a batch can take. */
 #define FD_WARM_MAX (16UL<<20)
-static hipError_t fd_stream_warm( hipStream_t st, fd_ed25519_gpu_slot * sl, unsigned long cap ) {
+static hipError_t fd_stream_warm( hipStream_t st, fd_ed25519_gpu_slot * sl, unsigned long cap, unsigned long max_sigs ) {
   hipError_t e;
+  unsigned long osz = max_sigs * sizeof(int32_t) < 64UL ? max_sigs * sizeof(int32_t) : 64UL;   /* d_out / h_out hold max_sigs codes */
   unsigned long top = cap < FD_WARM_MAX ? cap : FD_WARM_MAX;
   for( unsigned long sz=64UL; ; sz<<=3 ) {
     if( sz > top ) sz = top;
     if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, sz, hipMemcpyHostToDevice, st )) != hipSuccess ) return e;
     if( sz == top ) break;
   }
-  if( (e = hipMemsetAsync( sl->d_out, 0, 64, st )) != hipSuccess ) return e;
-  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, 64, hipMemcpyDeviceToHost, st )) != hipSuccess ) return e;
+  if( (e = hipMemsetAsync( sl->d_out, 0, osz, st )) != hipSuccess ) return e;
+  if( (e = hipMemcpyAsync( sl->h_out, sl->d_out, osz, hipMemcpyDeviceToHost, st )) != hipSuccess ) return e;
   return hipStreamSynchronize( st );
 }
 
@@ -246,7 +247,7 @@ static void fd_cu_groups_make( fd_ed25519_gpu_t * g, int groups ) {
        all 256 physical CUs from every group -- no isolation at all */
     for( int c=0; c<ncu; c++ ) if( c / (ncu / groups) == s % groups ) mask[c >> 5] |= 1u << (c & 31);
     if( hipExtStreamCreateWithCUMask( &g->slot[s].mstream, (uint32_t)words, mask ) != hipSuccess
-        || fd_stream_warm( g->slot[s].mstream, &g->slot[s], g->blob_cap ) != hipSuccess ) {
+        || fd_stream_warm( g->slot[s].mstream, &g->slot[s], g->blob_cap, g->max_sigs ) != hipSuccess ) {
       (void)hipGetLastError();
       for( int k=0; k<g->depth; k++ ) if( g->slot[k].mstream ) { hipStreamDestroy( g->slot[k].mstream ); g->slot[k].mstream = NULL; }
       g->mask_max = 0UL; g->groups = 1;
@@ -312,7 +313,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
     HIPCHK( hipEventCreateWithFlags( &sl->done, hipEventDisableTiming ) );
     sl->ticket = 0;
     memset( sl->h_blob, 0, blob_cap < FD_WARM_MAX ? blob_cap : FD_WARM_MAX );   /* the warm copies land zeros (d_blob stays zeroed) */
-    HIPCHK( fd_stream_warm( sl->stream, sl, blob_cap ) );
+    HIPCHK( fd_stream_warm( sl->stream, sl, blob_cap, max_sigs ) );
   }
   /* CU groups for small ring batches.  A 4,096-signature batch on the
      latency schedule is lone waves (256 quad-DSM waves, 192 front-end

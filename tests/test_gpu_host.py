@@ -144,3 +144,15 @@ def test_synth_producer_codes(ref, period_ns):
     assert (st["t_push_ns"] <= st["t_submit_ns"]).all() and (st["t_submit_ns"] <= st["t_done_ns"]).all()
     if period_ns:
         assert (np.diff(st["t_sched_ns"].astype(np.int64)) == period_ns).all()
+
+
+@pytest.mark.parametrize("cap", [1, 3, 15])
+def test_tiny_engine(ref, cap):
+    """Engines of a few signatures' capacity create and verify (engine
+    creation warms every slot stream with copies sized to the slot's own
+    buffers: the code buffer of a 1-signature engine is 4 bytes)."""
+    b = corpus.adversarial(cap, 120, seed=40 + cap, invalid_frac=0.5)
+    exp = oracle_batch(ref, b)
+    e = fa.Engine(0, cap, 1 << 16, depth=2)
+    assert (e.verify_packed(b.blob, b.desc) == exp).all()
+    e.close()

@@ -9,8 +9,10 @@ dispatch's counters are its own (rocprofv3 --pmc serialises dispatches).
   n = 16384  1,024 waves: one per SIMD on every SIMD
   n = 32768  2,048 waves: the quad (34.6 KiB of LDS) runs them in two
              rounds of one per SIMD
+  oct n <= 64: the per-signature drop-in's eight-lane DSM (fd_k_dsm_oct),
+             n / 8 waves
 
-usage: pmc_ring.py quad <n> [reps]"""
+usage: pmc_ring.py quad|oct <n> [reps]"""
 import math
 import os
 import sys
@@ -32,8 +34,11 @@ def main():
     b.desc = b.desc[:n]
     eng = fa.Engine(0, max_sigs=n, max_blob=max(len(b.blob), 1 << 24), depth=1)
     eng.dsm_quad_max = max(eng.dsm_quad_max, n)
-    if sched != "quad":
-        raise SystemExit("only the quad schedule remains (round 4)")
+    if sched == "oct":
+        if n > eng.dsm_oct_max:
+            raise SystemExit("the eight-lane DSM takes batches of at most dsm_oct_max")
+    elif sched != "quad":
+        raise SystemExit("schedules: quad, oct (round 4)")
     dev = torch.device("cuda", 0)
     d_blob = torch.from_numpy(np.concatenate([b.blob, np.zeros(64, np.uint8)])).to(dev)
     d_desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
