@@ -1044,6 +1044,17 @@ static unsigned long       fd_default_blob = 1UL << 26;
 
 static fd_ed25519_gpu_t * fd_default_engine( void );
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_default( void ) { return fd_default_engine(); }
+/* group-commit leaders of fd_ed25519_verify = the default engine's ring
+   depth (experiments: FD_ED25519_GPU_VQ_LEADERS, 1..FD_GPU_DEPTH_MAX) */
+static int fd_vq_leaders( void ) {
+  static int n = 0;
+  if( !n ) {
+    char const * e = getenv( "FD_ED25519_GPU_VQ_LEADERS" );
+    int v = e ? atoi( e ) : FD_GPU_DEPTH_DEFAULT;
+    n = v < 1 ? 1 : v > FD_GPU_DEPTH_MAX ? FD_GPU_DEPTH_MAX : v;
+  }
+  return n;
+}
 
 /* The default engine is released at exit, ahead of the HIP runtime's own
    teardown (its destructors were registered when it loaded, so they run
@@ -1061,7 +1072,7 @@ static fd_ed25519_gpu_t * fd_default_engine( void ) {
   std::lock_guard<std::mutex> guard( fd_default_lock );
   if( !fd_default_gpu ) {
     char const * dev = getenv( "FD_ED25519_GPU_DEVICE" );
-    fd_default_gpu = fd_ed25519_gpu_new( dev ? atoi( dev ) : 0, fd_default_sigs, fd_default_blob );
+    fd_default_gpu = fd_ed25519_gpu_new_ex( dev ? atoi( dev ) : 0, fd_default_sigs, fd_default_blob, fd_vq_leaders() );
     static int fini_set = 0;
     if( fd_default_gpu && !fini_set ) { fini_set = 1; atexit( fd_default_engine_fini ); }
   }
@@ -1166,10 +1177,10 @@ extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned
 
 /* fd_ed25519_verify (fd_ed25519.h:96-101): one signature per call.  Calls
    from several threads coalesce into shared batches (group commit): a call
-   joins the queue; if fewer than FD_VQ_LEADERS batches are running it
+   joins the queue; if fewer than fd_vq_leaders() batches are running it
    leads -- it takes every queued call (up to FD_VQ_MAX) as one batch on
    the process-default engine, hands each call its own code and wakes the
-   rest; a call arriving while FD_VQ_LEADERS batches run waits and rides
+   rest; a call arriving while fd_vq_leaders() batches run waits and rides
    the next one.  Leaders' batches run side by side on the engine's ring
    slots (fd_run_ptr_batch holds the engine lock only to take a slot,
    enqueue and collect), so a call that arrives while another batch is in
@@ -1178,7 +1189,6 @@ extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned
    batch ahead of it (p50 0.95 ms for a 0.46 ms round trip,
    profiles/r03_per_signature_threads.jsonl). */
 #define FD_VQ_MAX     4096UL
-#define FD_VQ_LEADERS 3        /* the default engine's ring depth (FD_GPU_DEPTH_DEFAULT) */
 struct fd_vreq { uint8_t const * m; unsigned long sz; uint8_t const * s; uint8_t const * p; int out; int done; };
 static std::mutex              fd_vq_lock;
 static std::condition_variable fd_vq_cv;
@@ -1209,7 +1219,7 @@ extern "C" int fd_ed25519_verify( void const * msg, unsigned long sz, void const
   fd_vq.push_back( &me );
   while( !me.done ) {
     /* lead only while this call is still queued (a leader may have taken it) */
-    if( fd_vq_running >= FD_VQ_LEADERS || fd_vq.empty() ) { fd_vq_cv.wait( lk ); continue; }
+    if( fd_vq_running >= fd_vq_leaders() || fd_vq.empty() ) { fd_vq_cv.wait( lk ); continue; }
     fd_vq_running++;
     std::vector<fd_vreq *> b;
     while( !fd_vq.empty() && b.size() < FD_VQ_MAX ) { b.push_back( fd_vq.front() ); fd_vq.pop_front(); }
