@@ -948,6 +948,62 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
 #define FD_QMUL fd_fe_mul
 #endif
 
+/* The lane-split DSMs' prologue reads, all issued before any is used (a
+   lone wave otherwise pays one memory round trip per dependent load: the
+   status, then the point states, then op_start, then per-iteration waits
+   in the op-row and Bi copies -- ~10 us of the single-signature DSM):
+   the signature's code by the reference's error precedence
+   (fd_ed25519_user.c:372-403) and its first op. */
+FD_QDEV int fd_lat_code( int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
+                         int32_t const * __restrict__ op_start, uint64_t n, uint64_t ii, int live, int & start ) {
+  int st = status[ii], pa = pstat[ii], pr = pstat[n+ii], os = op_start[ii];
+  /* value barriers: all four loads in flight together (LLVM otherwise
+     sinks the point-state loads into the branch that first uses them) */
+  st = fd_opaque( st ); pa = fd_opaque( pa ); pr = fd_opaque( pr ); os = fd_opaque( os );
+  int code;
+  if( st != FD_ST_PENDING )                        code = st;
+  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
+  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
+  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
+  else                                             code = FD_ST_PENDING;
+  start = (live && code == FD_ST_PENDING) ? os : FD_OPS_MAX;
+  return code;
+}
+/* a wave's signature-major op rows (from chunk t0/16 on) and the Bi table
+   into LDS: every lane's loads first, then its stores.  SIGS rows of
+   FD_OPS_MAX bytes in 16-byte chunks; bi: 8 entries in the kernel's layout
+   (bi_at maps a Bi dword index to its LDS dword index) */
+template<int SIGS, int BI_DW, typename AT>
+FD_QDEV void fd_lat_stage( uint8_t const * __restrict__ ops, uint64_t sig0, uint64_t n, int t0,
+                           uint8_t (*lops)[FD_QOPS_ROW], int32_t * lbi, AT bi_at ) {
+  uint32_t const lane = threadIdx.x & 63u;
+  int const c0 = t0 >> 4;
+  constexpr int NC = (SIGS*(FD_OPS_MAX/16) + 63) / 64, NB = (BI_DW + 63) / 64;
+  int4 v[NC];
+#pragma unroll
+  for( int j=0; j<NC; j++ ) {
+    int c = (int)lane + 64*j, sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
+    uint64_t gs = sig0 + (uint64_t)sg;
+    /* unconditional loads (a row of this batch either way), selected after:
+       no branch, so no wait between them */
+    uint64_t const gl = gs < n ? gs : n - 1u;
+    int4 x = *(int4 const *)(ops + gl*FD_OPS_MAX + (uint64_t)(ch < FD_OPS_MAX/16 ? ch : 0)*16u);
+    bool const use = c < SIGS*(FD_OPS_MAX/16) && ch >= c0 && gs < n;
+    v[j] = make_int4( use ? x.x : 0, use ? x.y : 0, use ? x.z : 0, use ? x.w : 0 );
+  }
+  int32_t b[NB];
+#pragma unroll
+  for( int j=0; j<NB; j++ ) { int k = (int)lane + 64*j; b[j] = k < BI_DW ? fd_gpu_bi_tab[bi_at.src( k )] : 0; }
+#pragma unroll
+  for( int j=0; j<NC; j++ ) {
+    int c = (int)lane + 64*j, sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
+    if( c < SIGS*(FD_OPS_MAX/16) && ch >= c0 ) *(int4 *)&lops[sg][ch*16] = v[j];
+  }
+#pragma unroll
+  for( int j=0; j<NB; j++ ) { int k = (int)lane + 64*j; if( k < BI_DW ) lbi[bi_at.dst( k )] = b[j]; }
+}
+struct fd_bi_quad { __device__ __forceinline__ int src( int k ) const { return k; } __device__ __forceinline__ int dst( int k ) const { return k; } };
+
 FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                            int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
                            int32_t * __restrict__ out, int strict, fd_quad_lds & L ) {
@@ -958,19 +1014,9 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   int live = i < n;
   uint64_t ii = live ? i : 0;
   uint64_t m = 2*n;
-  int st = status[ii];
-  int pa = pstat[ii], pr = pstat[n+ii];
-  int code;
-  /* error precedence (fd_ed25519_user.c:372-403) */
-  if( st != FD_ST_PENDING )                        code = st;
-  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
-  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
-  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
-  else                                             code = FD_ST_PENDING;
-  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
-
   /* lane q of vr = [Z, Y, -X, -T] of A (fd_ed25519_user.c:408-409), and
-     this lane's half of the final compare's (r.x, r.y) */
+     this lane's half of the final compare's (r.x, r.y); loaded first, so
+     they are in flight with the status reads below */
   uint32_t const comp = q==0u ? 20u : q==1u ? 10u : q==2u ? 0u : 30u;
   fe r, rr;
 #pragma unroll
@@ -979,6 +1025,8 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     r.v[k]  = q >= 2u ? (int32_t)(0u - (uint32_t)x) : x;
     rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
   }
+  int start;
+  int code = fd_lat_code( status, pstat, op_start, n, ii, live, start );
 
   /* op streams of the wave's 16 signatures (signature-major in HBM) ->
      LDS as 16-byte pieces from the wave's first op on: at most 8
@@ -986,17 +1034,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      ~100-deep chain of dependent round trips in front of the first step) */
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
-  {
-    int const c0 = t0 >> 4;
-    for( int c=(int)lane; c<FD_QSIGS*(FD_OPS_MAX/16); c+=64 ) {
-      int sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
-      if( ch < c0 ) continue;
-      uint64_t gs = sig0 + (uint64_t)sg;
-      int4 v = gs < n ? *(int4 const *)(ops + gs*FD_OPS_MAX + (uint64_t)ch*16u) : make_int4( 0, 0, 0, 0 );
-      *(int4 *)&L.ops[sg][ch*16] = v;
-    }
-    for( int k=lane; k<8*FD_TAB_ENTRY; k+=64 ) L.tab[FD_QSIGS][k] = fd_gpu_bi_tab[k];
-  }
+  fd_lat_stage<FD_QSIGS, 8*FD_TAB_ENTRY>( ops, sig0, n, t0, L.ops, L.tab[FD_QSIGS], fd_bi_quad{} );
 
   /* per-lane constant masks */
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
@@ -1391,6 +1429,12 @@ FD_QDEV void fd_o_tab_store( int32_t * p, fh const & x ) {
   ((int4 *)p)[0] = make_int4( x.v[0], x.v[1], x.v[2], x.v[3] ); ((int4 *)p)[1] = make_int4( x.v[4], 0, 0, 0 );
 }
 
+/* Bi dword k (entry e, lane l, limb) from the quad layout into the oct's
+   half-aligned one (limbs 0-4 | 3 pad | limbs 5-9) */
+struct fd_bi_oct {
+  __device__ __forceinline__ int src( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_TAB_ENTRY + l*FD_TAB_LANE + limb; }
+  __device__ __forceinline__ int dst( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_OTAB_ENTRY + l*FD_OTAB_LANE + (limb < 5 ? limb : limb + 3); }
+};
 struct fd_oct_lds {
   int32_t tab[FD_OSIGS+1][8*FD_OTAB_ENTRY];   /* Ai per signature, [FD_OSIGS] = Bi */
   uint8_t ops[FD_OSIGS][FD_QOPS_ROW];
@@ -1409,17 +1453,6 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   int live = i < n;
   uint64_t ii = live ? i : 0;
   uint64_t m = 2*n;
-  int st = status[ii];
-  int pa = pstat[ii], pr = pstat[n+ii];
-  int code;
-  /* error precedence (fd_ed25519_user.c:372-403), as the quad */
-  if( st != FD_ST_PENDING )                        code = st;
-  else if( pa == FD_PT_BAD || pr == FD_PT_BAD )    code = FD_ED25519_ERR_PUBKEY;
-  else if( pa == FD_PT_SMALL )                     code = FD_ED25519_ERR_PUBKEY;
-  else if( pr == FD_PT_SMALL )                     code = FD_ED25519_ERR_SIG;
-  else                                             code = FD_ST_PENDING;
-  int start = (live && code == FD_ST_PENDING) ? op_start[ii] : FD_OPS_MAX;
-
   uint32_t const comp = q==0u ? 20u : q==1u ? 10u : q==2u ? 0u : 30u;
   fe r, rr;
 #pragma unroll
@@ -1428,24 +1461,12 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
     r.v[k]  = q >= 2u ? (int32_t)(0u - (uint32_t)x) : x;
     rr.v[k] = pts[(uint64_t)((q==1u ? 10u : 0u)+k)*m + n + ii];
   }
+  int start;
+  int code = fd_lat_code( status, pstat, op_start, n, ii, live, start );   /* as the quad, after the point loads */
 
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
-  {
-    int const c0 = t0 >> 4;
-    for( int c=(int)lane; c<FD_OSIGS*(FD_OPS_MAX/16); c+=64 ) {
-      int sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
-      if( ch < c0 ) continue;
-      uint64_t gs = sig0 + (uint64_t)sg;
-      int4 v = gs < n ? *(int4 const *)(ops + gs*FD_OPS_MAX + (uint64_t)ch*16u) : make_int4( 0, 0, 0, 0 );
-      *(int4 *)&L.ops[sg][ch*16] = v;
-    }
-    /* Bi into the half-aligned entry layout */
-    for( int k=lane; k<8*4*10; k+=64 ) {
-      int e = k / 40, l = (k / 10) % 4, limb = k % 10;
-      L.tab[FD_OSIGS][e*FD_OTAB_ENTRY + l*FD_OTAB_LANE + (limb < 5 ? limb : limb + 3)] = fd_gpu_bi_tab[e*FD_TAB_ENTRY + l*FD_TAB_LANE + limb];
-    }
-  }
+  fd_lat_stage<FD_OSIGS, 8*4*10>( ops, sig0, n, t0, L.ops, L.tab[FD_OSIGS], fd_bi_oct{} );
 
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
   uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
