@@ -423,3 +423,23 @@ def test_oct_equals_uniform_forced(oct, uniform, n):
     o = oct.verify_packed(base.blob, base.desc)
     u = uniform.verify_packed(base.blob, base.desc)
     assert (o == u).all(), np.nonzero(o != u)[0][:10]
+
+
+@pytest.mark.parametrize("n", [1, 5, 32, 33])
+def test_small_batches_s_recoded_ahead(engine, ref, n):
+    """Batches of at most 32 have S's digits recoded ahead on an idle front-end
+    wave (fd_sdig_body) and the prep wave runs only k's pass; S at or above
+    2^252 that still passes the range check (S = L - 1 .. L - 3) is skipped
+    there and recoded by prep itself, in the same wave as lanes that take
+    the digits ahead.  Codes equal the reference's; n = 33 is one past the
+    offload."""
+    b = corpus.adversarial(n, 150, seed=300 + n, invalid_frac=0.0)
+    L = corpus.L
+    for j in range(1, n, 4):      # every fourth signature: S just below L
+        so = int(b.desc[j]["sig_off"])
+        b.blob[so + 32:so + 64] = np.frombuffer((L - 1 - (j % 3)).to_bytes(32, "little"), np.uint8)
+    exp = oracle_batch(ref, b)
+    for rep in range(3):          # repeated launches reuse the scratch with new tags
+        got = engine.verify_packed(b.blob, b.desc)
+        assert (got == exp).all(), (rep, np.nonzero(got != exp)[0][:10], got[:8], exp[:8])
+    assert (exp == 0).sum() >= n - (n + 2) // 4
