@@ -92,6 +92,39 @@ PEAK_CLOCK_GHZ = 2.4
 PEAK_INT32_OPS = 256 * 4 * 32 * PEAK_CLOCK_GHZ * 1e9   # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T slots/s
 
 
+# algorithmic HBM bytes per verify (the txn bytes a signature
+# brings, its descriptor and its code)
+ALGO_BYTES_PER_SIG = 1260
+
+
+def lib_sha16(path):
+    """first 16 hex digits of the sha256 of a library file"""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def load_traffic(path, n_step, kernel, sha):
+    """roofline.traffic from a PMC summary (tools/pmc_summary.py), only if it
+    was measured on THIS library build and launch size: a summary of another
+    build describes kernels that may no longer exist (round-4 verdict)."""
+    if not os.path.exists(path):
+        return None, "no PMC summary"
+    try:
+        tr = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "unreadable PMC summary"
+    if tr.get("lib_sha16") != sha:
+        return None, f"stale: PMC summary of library {tr.get('lib_sha16')}, loaded {sha}"
+    if tr.get("sigs_per_launch") != n_step:
+        return None, f"PMC summary of {tr.get('sigs_per_launch')} signatures per launch, this run {n_step}"
+    v = tr.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    return v, ("current" if v is not None else f"no FETCH/WRITE for {kernel}")
+
+
 def sha_blocks(msg_sz):
     return (64 + msg_sz + 17 + 127) // 128
 
@@ -115,6 +148,8 @@ def parse():
     ap.add_argument("--dry-cpu", action="store_true", help="rehearse the multi-rank plumbing on the CPU (tests only)")
     ap.add_argument("--cpu-sample", type=int, default=393216, help="signatures in the CPU baseline sample (~15 thread-s of reference work)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--stream-batches", type=int, default=48,
+                    help="batches of the PCIe-inclusive large-batch C2 leg (c2_streamed)")
     return ap.parse_args()
 
 
@@ -182,19 +217,29 @@ def cpu_baseline(batch, nsig, threads):
     return res
 
 
-def reference_check(batch, got, threads):
-    """The reference's fd_ed25519_verify (oracle/_ref/libfdref.so) over every
-    signature of the step corpus, code by code against the engine's codes of
-    the first step.  The checker only: nothing timed goes through it."""
+def step_reference_codes(batch, threads):
+    """The reference build's codes for every signature of the step corpus
+    (the checker, run after the timed region; None if it was not shipped)."""
     import ctypes
     ref = os.path.join(ROOT, "oracle", "_ref", "libfdref.so")
     if not os.path.exists(ref):
-        return {"checked": False, "note": "reference build not shipped"}
+        return None
     sig, pub, data, off, sz = batch.flat()
     exp = np.zeros(len(batch), np.int32)
     P = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    t0 = time.time()
     ctypes.CDLL(ref).ref_verify_batch(ctypes.c_uint64(len(batch)), P(sig), P(pub), P(data), P(off), P(sz), P(exp), threads)
+    return exp
+
+
+def reference_check(batch, got, threads, exp=None):
+    """The reference's fd_ed25519_verify (oracle/_ref/libfdref.so) over every
+    signature of the step corpus, code by code against the engine's codes of
+    the first step.  The checker only: nothing timed goes through it."""
+    t0 = time.time()
+    if exp is None:
+        exp = step_reference_codes(batch, threads)
+    if exp is None:
+        return {"checked": False, "note": "reference build not shipped"}
     mism = int((exp != got[:len(batch)]).sum())
     return {"checked": True, "sigs": len(batch), "mismatches": mism, "reference_codes": codes_hist(exp),
             "seconds": time.time() - t0, "checker": "oracle/_ref/libfdref.so (reference AVX2 build)"}
@@ -407,14 +452,7 @@ def main():
             kern[name] = {"ms": float(ms), "achieved_Tops": ach, "frac": ach * 1e12 / PEAK_INT32_OPS,
                           "ms_serial": float(ms1), "frac_serial": ach1 * 1e12 / PEAK_INT32_OPS}
         dom = max(kern, key=lambda k: kern[k]["ms_serial"])     # the kernel with the most work
-        traffic = None
-        if os.path.exists(a.traffic):
-            try:
-                tr = json.load(open(a.traffic))
-                if tr.get("sigs_per_launch") == n_step:
-                    traffic = tr.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        traffic, traffic_status = load_traffic(a.traffic, n_step, dom, lib_sha16(fa.LIB_PATH))
         w_total = SLOTS_DSM + SLOTS_DECOMP + SLOT_SHA_BLOCK * blocks + SLOTS_PREP_FIXED
         res["roofline"] = {
             "bound": "valu-int32",
@@ -424,6 +462,12 @@ def main():
             "unit": "Tint32op/s",
             "frac": kern[dom]["frac"],
             "traffic": traffic,
+            # HBM bytes the kernel moved / the path's algorithmic bytes for the
+            # signatures of one launch (1.26 KB per verify -- the
+            # txn bytes, descriptors and codes; every intermediate stays on chip
+            # in the model)
+            "traffic_ratio": None if traffic is None else traffic / (ALGO_BYTES_PER_SIG * n_step),
+            "traffic_status": traffic_status,
             "per_kernel": kern,
             "pipeline_frac": value * w_total / PEAK_INT32_OPS,
             # the shader clock the pool ran at over the timed launches (s_memtime vs
@@ -443,7 +487,8 @@ def main():
                           "(MAC and 64-bit ops 2, int32 op 1); peak = 78.6 T full-rate int32 lane-op "
                           "slots/s (DESIGN.md section 4)",
             "traffic_note": "HBM bytes per launch of the dominant kernel from rocprofv3 PMC "
-                            "(2*FETCH_SIZE + WRITE_SIZE, profiles/pmc_traffic.json); the path is "
+                            "(2*FETCH_SIZE + WRITE_SIZE, profiles/pmc_traffic.json, used only when "
+                            "its recorded library hash equals the loaded library's); the path is "
                             "VALU-bound, traffic is a secondary check",
         }
         if not a.no_latency:
@@ -457,11 +502,23 @@ def main():
             res["ring_4096_verifies_per_s"] = lat["pcie_inclusive_verifies_per_s"]
             res["ring_4096_best_verifies_per_s_at_p99_le_1ms"] = (lat["best_under_p99_1ms"] or {}).get("verifies_per_s")
             res["ring_4096_max_offered_at_sched_p99_le_1ms"] = lat["max_offered_at_sched_p99_le_1ms"]
+        step_codes = d_out.cpu().numpy()
+        exp_step = step_reference_codes(batch, usable_cores())
+        if not a.no_latency:
+            # the deployable C2 number: the same step corpus streamed from host
+            # memory through the feeder and the registered ring at pool
+            # granularity, PCIe both ways included (the `value` is HBM-resident)
+            big = ring_stream(fa, batch, local, a.stream_batches, 3, window=3, expected=exp_step,
+                              batch_sigs=STREAM_BATCH_SIGS, q2_at=())
+            big["content"] = ("the step corpus (C2: 1232-byte txns, 1-2 sigs/txn), batches of "
+                              f"{STREAM_BATCH_SIGS} signatures DMA'd from a registered host region, codes to the host")
+            res["c2_streamed"] = big
+            res["c2_streamed_large_batch_verifies_per_s"] = big["pcie_inclusive_verifies_per_s"] if big["codes_ok"] else None
         if not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(base, a.cpu_sample, usable_cores())
             # the checker: the reference build's codes for the whole step corpus
             # vs the engine's (the rejects above are the reference's own)
-            res["reference_check"] = reference_check(batch, d_out.cpu().numpy(), usable_cores())
+            res["reference_check"] = reference_check(batch, step_codes, usable_cores(), exp_step)
         res["corpus_gen_s"] = gen_s
 
     if rank == 0:
@@ -476,6 +533,8 @@ def main():
 # them), so every timed ring batch carries reference evidence
 RING_WINDOWS = 64
 RING_Q2_AT = (1024, 2048, 4095)
+# the PCIe-inclusive C2 leg at pool granularity (c2_streamed)
+STREAM_BATCH_SIGS = 262144
 # offered loads of the open-loop sweep, M verifies/s
 PACED_MPS = (25, 30, 32, 34, 36, 38, 40)
 
@@ -548,7 +607,7 @@ def latency_legs(fa, corpus, a, device):
 
 
 def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, period_ns=0,
-                expected=None):
+                expected=None, batch_sigs=BATCH_SIGS, q2_at=RING_Q2_AT):
     """C2 at its own granularity: nb 4096-signature batches streamed through
     one engine's pinned ring by its per-GPU feeder thread
     (fd_ed25519_gpu_feeder: NUMA-pinned, whole ring in flight), PCIe both
@@ -563,32 +622,54 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
     starts[i % 64] of `base` (one batch per BATCH_SIGS-signature window);
     every code is returned and, with `expected` (the reference build's codes
     for `base`), compared code by code after the timed run."""
-    eng = fa.Engine(device, max_sigs=BATCH_SIGS, max_blob=8 << 20, depth=depth)
+    BS = batch_sigs
+    nwin = len(base) // BS
+    # the largest blob span of a window (a batch moves one span)
+    span = 8 << 20
+    for w in range(nwin):
+        d = base.desc[w * BS:(w + 1) * BS]
+        lo = int(min(d["sig_off"].min(), d["pub_off"].min(), d["msg_off"].min()))
+        hi = int(max((d["sig_off"].astype(np.int64) + 64).max(), (d["pub_off"].astype(np.int64) + 32).max(),
+                     (d["msg_off"].astype(np.int64) + d["msg_sz"]).max()))
+        span = max(span, hi - lo + 64)
+    eng = fa.Engine(device, max_sigs=BS, max_blob=span, depth=depth)
     try:
         if groups:
             eng.cu_groups = groups
         if register:
             eng.register(base.blob)
         feeder = fa.Feeder(eng)
-        nwin = len(base) // BATCH_SIGS
-        starts = np.random.default_rng(seed).permutation(nwin).astype(np.uint64) * BATCH_SIGS
+        starts = np.random.default_rng(seed).permutation(nwin).astype(np.uint64) * BS
         W = window or depth
         t0 = time.perf_counter()
-        st, codes = feeder.synth(base.blob, base.desc, BATCH_SIGS, starts, nb, W, period_ns, codes=True)
+        st, codes = feeder.synth(base.blob, base.desc, BS, starts, nb, W, period_ns, codes=True)
         wall = time.perf_counter() - t0
         numa = feeder.numa_node
         feeder.close()
         # the codes of EVERY batch (fill included) against the reference
         c = st["codes"].sum(axis=0)
         hist = {k: int(v) for k, v in zip(("0", "-1", "-2", "-3", "other"), c) if v or k == "0"}
-        complete = bool((st["state"] == 1).all()) and int(c.sum()) == nb * BATCH_SIGS and int(c[4]) == 0
+        complete = bool((st["state"] == 1).all()) and int(c.sum()) == nb * BS and int(c[4]) == 0
         mism = None
+        label_mism = None
         if expected is not None:
             mism = 0
             for s in range(min(len(starts), nb)):
                 rows = codes[s::len(starts)]
                 o = int(starts[s])
-                mism += int((rows != expected[o:o + BATCH_SIGS][None, :]).sum())
+                mism += int((rows != expected[o:o + BS][None, :]).sum())
+        elif base.label is not None:
+            # no reference build on this box: the corpus's own labels, which
+            # decide only the untouched signatures (valid, label 0, off the
+            # Q2 offsets) -- a partial check, so codes_ok stays None
+            label_mism = 0
+            keep = np.ones(BS, bool)
+            keep[list(q2_at)] = False
+            for s in range(min(len(starts), nb)):
+                rows = codes[s::len(starts)]
+                o = int(starts[s])
+                v = (base.label[o:o + BS] == 0) & keep
+                label_mism += int((rows[:, v] != 0).sum())
         skip = W if nb > 2 * W else 0          # the ring's fill
         st = st[skip:]
         lat = (st["t_done_ns"] - st["t_push_ns"]) * 1e-6
@@ -596,10 +677,10 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         hop = (st["t_submit_ns"] - st["t_push_ns"]) * 1e-6
         pick = (st["t_pick_ns"] - st["t_push_ns"]) * 1e-6      # the feeder's pickup
         enq = (st["t_submit_ns"] - st["t_pick_ns"]) * 1e-6     # staging + HIP enqueue of the batch
-        res = {"batch_sigs": BATCH_SIGS, "batches": nb, "ring_depth": depth, "window": W,
+        res = {"batch_sigs": BS, "batches": nb, "ring_depth": depth, "window": W,
                "cu_groups": eng.cu_groups, "registered_source": bool(register),
                "feeder_numa_node": numa, "producer": "native (fd_ed25519_gpu_feeder_synth)",
-               "pcie_inclusive_verifies_per_s": nb * BATCH_SIGS / wall,
+               "pcie_inclusive_verifies_per_s": nb * BS / wall,
                "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
                "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
                "submit_to_done_p50_ms": float(np.percentile(qlat, 50)),
@@ -609,10 +690,12 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                "push_to_pick_p50_ms": float(np.percentile(pick, 50)), "push_to_pick_p99_ms": float(np.percentile(pick, 99)),
                "pick_to_submit_p50_ms": float(np.percentile(enq, 50)), "pick_to_submit_p99_ms": float(np.percentile(enq, 99)),
                "codes": hist, "reference_checked": expected is not None, "mismatches": mism,
-               "codes_ok": complete and (mism == 0 if expected is not None else True)}
+               "label_check_mismatches": label_mism,
+               # True only when every code was compared with the reference build's
+               "codes_ok": (complete and mism == 0) if expected is not None else (False if not complete else None)}
         if period_ns:
             sl = (st["t_done_ns"] - st["t_sched_ns"]) * 1e-6
-            offered = BATCH_SIGS / (period_ns * 1e-9)
+            offered = BS / (period_ns * 1e-9)
             res.update(offered_verifies_per_s=offered,
                        sustained=res["pcie_inclusive_verifies_per_s"] >= 0.98 * offered,
                        sched_to_done_p50_ms=float(np.percentile(sl, 50)),

@@ -138,25 +138,34 @@ FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return fd_opaque64( c
 
 /* limbs from the absorbed-chain column sums (S2, S6, S8 with their
    carry-ins added): round-two carries c3 -> limb 4, 19 c9 -> limb 0, the
-   residuals, the biases removed */
-FD_DEV void fd_fe_limbs( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, int64_t S3, int64_t S4,
-                         int64_t S5, int64_t S6, int64_t S7, int64_t S8, int64_t S9 ) {
+   residuals, the biases removed.  BIASED = 1 leaves each limb's bias in
+   (limb k + 2^25 for even k, + 2^24 for odd k: one instruction fewer per
+   limb); a consumer that folds the bias into a constant it adds anyway
+   takes these (the quad DSM's operand and output mixes). */
+template<int BIASED>
+FD_DEV void fd_fe_limbs_t( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, int64_t S3, int64_t S4,
+                           int64_t S5, int64_t S6, int64_t S7, int64_t S8, int64_t S9 ) {
   int64_t c3 = S3 >> 25, c9 = S9 >> 25;
   uint32_t const m26 = (1u<<26)-1u, m25 = (1u<<25)-1u;
+  uint32_t const be = BIASED ? 0u : (1u<<25), bo = BIASED ? 0u : (1u<<24);
   int64_t  V4  = (int64_t)((uint32_t)S4 & m26) + c3;       /* limb 4: second carry */
   uint32_t c4b = (uint32_t)(V4 >> 26);
   int64_t  V0  = (int64_t)((uint32_t)S0 & m26) + c9*19;    /* limb 0: second carry */
   uint32_t c0b = (uint32_t)(V0 >> 26);
-  out.v[0] = fd_opaque( (int32_t)(((uint32_t)V0 & m26)       - (1u<<25)) );
-  out.v[1] = fd_opaque( (int32_t)(((uint32_t)S1 & m25) + c0b - (1u<<24)) );
-  out.v[2] = fd_opaque( (int32_t)(((uint32_t)S2 & m26)       - (1u<<25)) );
-  out.v[3] = fd_opaque( (int32_t)(((uint32_t)S3 & m25)       - (1u<<24)) );
-  out.v[4] = fd_opaque( (int32_t)(((uint32_t)V4 & m26)       - (1u<<25)) );
-  out.v[5] = fd_opaque( (int32_t)(((uint32_t)S5 & m25) + c4b - (1u<<24)) );
-  out.v[6] = fd_opaque( (int32_t)(((uint32_t)S6 & m26)       - (1u<<25)) );
-  out.v[7] = fd_opaque( (int32_t)(((uint32_t)S7 & m25)       - (1u<<24)) );
-  out.v[8] = fd_opaque( (int32_t)(((uint32_t)S8 & m26)       - (1u<<25)) );
-  out.v[9] = fd_opaque( (int32_t)(((uint32_t)S9 & m25)       - (1u<<24)) );
+  out.v[0] = fd_opaque( (int32_t)(((uint32_t)V0 & m26)       - be) );
+  out.v[1] = fd_opaque( (int32_t)(((uint32_t)S1 & m25) + c0b - bo) );
+  out.v[2] = fd_opaque( (int32_t)(((uint32_t)S2 & m26)       - be) );
+  out.v[3] = fd_opaque( (int32_t)(((uint32_t)S3 & m25)       - bo) );
+  out.v[4] = fd_opaque( (int32_t)(((uint32_t)V4 & m26)       - be) );
+  out.v[5] = fd_opaque( (int32_t)(((uint32_t)S5 & m25) + c4b - bo) );
+  out.v[6] = fd_opaque( (int32_t)(((uint32_t)S6 & m26)       - be) );
+  out.v[7] = fd_opaque( (int32_t)(((uint32_t)S7 & m25)       - bo) );
+  out.v[8] = fd_opaque( (int32_t)(((uint32_t)S8 & m26)       - be) );
+  out.v[9] = fd_opaque( (int32_t)(((uint32_t)S9 & m25)       - bo) );
+}
+FD_DEV void fd_fe_limbs( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, int64_t S3, int64_t S4,
+                         int64_t S5, int64_t S6, int64_t S7, int64_t S8, int64_t S9 ) {
+  fd_fe_limbs_t<0>( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
 }
 
 /* COL provides template<int K> int64_t col(int64_t init) const: init +
@@ -181,7 +190,7 @@ FD_DEV void fd_cols( COL const & c, int64_t & s1, int64_t & s2, int64_t & s3 ) {
   fd_cols_step<COL,K1,K2,K3,8>( c, s1, s2, s3 ); fd_cols_step<COL,K1,K2,K3,9>( c, s1, s2, s3 );
 }
 
-template<typename COL>
+template<typename COL, int BIASED=0>
 FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
   /* groups in carry order: {0,4,2} and {6,8} wait for no carry, 1 needs
      c0; {5,3} need c4 and c2 (after c1); 7 needs c6 (after c5); 9 needs
@@ -197,7 +206,7 @@ FD_DEV void fd_fe_chain( fd_gpu_fe_t & out, COL const & c ) {
   int64_t S7 = c.template col<7>( S6 >> 26 );
   S8 += S7 >> 25;
   int64_t S9 = c.template col<9>( S8 >> 26 );
-  fd_fe_limbs( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
+  fd_fe_limbs_t<BIASED>( out, S0, S1, S2, S3, S4, S5, S6, S7, S8, S9 );
 }
 
 /* Columns K1, K2 of two independent products A and B, the four multiply
@@ -364,6 +373,16 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
   fd_fe_pre_f( f2, f );
   fd_fe_pre_g( g19, g );
   fd_fe_mul_pre( h, f, f2, g, g19 );
+}
+
+/* h + bias (fd_fe_limbs_t<1>): the product with each limb's carry bias
+   left in, for consumers that fold it into a constant they add anyway */
+FD_DEV void fd_fe_mul_b( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const & g ) {
+  int32_t f2[10], g19[10];
+  fd_fe_pre_f( f2, f );
+  fd_fe_pre_g( g19, g );
+  fd_mul_cols c = { f.v, f2, g.v, g19 };
+  fd_fe_chain<fd_mul_cols, 1>( h, c );
 }
 
 /* h = f*g for a lone wave (the latency kernel): all ten column sums as

@@ -550,10 +550,29 @@ extern "C" unsigned long fd_ed25519_gpu_dsm_oct_max( fd_ed25519_gpu_t const * g 
 extern "C" unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * g ) { return g ? g->max_sigs : 0UL; }
 extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) { return g ? g->max_blob : 0UL; }
 
+/* Slots orphaned by a timed-out wait (a synchronous call, or a staged
+   per-signature chunk whose blocking poll gave up) come back once their
+   event completes.  Caller holds g->lock. */
+static void fd_reclaim_orphans( fd_ed25519_gpu_t * g ) {
+  for( int s=0; s<g->depth; s++ ) {
+    fd_ed25519_gpu_slot * sl = &g->slot[s];
+    if( sl->orphan && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->ticket = 0; sl->staged = 0; }
+  }
+}
+
+/* Give up on a submitted ticket nobody will poll again (its blocking poll
+   timed out): the slot is reclaimed by fd_reclaim_orphans once the batch
+   drains, instead of staying taken for the engine's lifetime. */
+static void fd_abandon_ticket( fd_ed25519_gpu_t * g, unsigned long ticket ) {
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket == ticket ) g->slot[s].orphan = 1;
+}
+
 /* Lend a free slot's pinned staging buffers (zero-copy submit). */
 extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
   if( !g || !blob || !desc ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
+  fd_reclaim_orphans( g );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
     if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->h_blob; *desc = sl->h_desc; return 0; }
@@ -570,10 +589,7 @@ extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob 
 /* a free slot: the staged one owning `blob` if any, else any unstaged one
    (slots orphaned by a timed-out synchronous call come back once done) */
 static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * blob ) {
-  for( int s=0; s<g->depth; s++ ) {
-    fd_ed25519_gpu_slot * sl = &g->slot[s];
-    if( sl->orphan && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->ticket = 0; }
-  }
+  fd_reclaim_orphans( g );
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && g->slot[s].h_blob == blob ) return &g->slot[s];
   if( g->groups > 1 ) {
     /* slot s runs on CU group s mod groups: of the free slots, take one on
@@ -1140,7 +1156,12 @@ static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsig
     int r = fd_ed25519_gpu_try_submit( g, cnt, hb, used, dd, &ticket );
     if( r != 1 ) { fd_ed25519_gpu_unstage( g, hb ); return r < 0 ? r : FD_ED25519_ERR_GPU; }
     r = fd_ed25519_gpu_poll( g, ticket, out + i, 1 );
-    if( r != 1 ) return r < 0 ? r : FD_ED25519_ERR_GPU;   /* timed out: the ticket stays valid, the slot is not reused */
+    if( r != 1 ) {
+      /* timed out or failed: nobody polls this ticket again, so its slot is
+         orphaned (reclaimed once the batch drains), not lost to the engine */
+      fd_abandon_ticket( g, ticket );
+      return r < 0 ? r : FD_ED25519_ERR_GPU;
+    }
     i += cnt;
   }
   return 0;

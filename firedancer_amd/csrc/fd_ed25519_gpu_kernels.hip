@@ -934,6 +934,9 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
 #ifndef FD_QUAD_ILP
 #define FD_QUAD_ILP 0
 #endif
+#ifndef FD_QUAD_V2
+#define FD_QUAD_V2 1   /* the step layout of fd_q2_kind_bits (round 5); 0 = round 4's */
+#endif
 #ifndef FD_QUAD_DPP_AND
 #define FD_QUAD_DPP_AND 1
 #endif
@@ -1075,8 +1078,14 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
-  uint64_t const okw = fd_op_kind_word( q );
   uint32_t const tab_bi = (uint32_t)(L.tab[FD_QSIGS] - tab_s);   /* int32s from this signature's Ai to Bi */
+#if FD_QUAD_V2
+  /* this lane's decode words for D, positive-digit add, negative-digit add
+     (fd_q2_kind_bits: the step's lane layout, masks and bias constants) */
+  uint32_t const kw0 = fd_q2_kind_bits( q, 0, 0 ), kw1 = fd_q2_kind_bits( q, 1, 0 ), kw2 = fd_q2_kind_bits( q, 1, 1 );
+#else
+  uint64_t const okw = fd_op_kind_word( q );
+#endif
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
@@ -1085,10 +1094,16 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
        any other row's bytes only steer lanes whose result is discarded
        (code != FD_ST_PENDING), with table indices bounded by the masks */
     int op = (int)L.ops[ls][t];
+#if FD_QUAD_V2
+    uint32_t const madd = fd_ok_mask( (uint32_t)op, 7 ), mneg = fd_ok_mask( (uint32_t)op, 5 );
+    uint32_t const kd = fd_sel( madd, fd_sel( mneg, kw2, kw1 ), kw0 );
+    uint32_t idx = fd_ok_bits( kd, FD_Q2_IDX, 2 );
+#else
     uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
     uint32_t add = fd_ok_mask( kd, FD_OK_QS );
     /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
     uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
+#endif
     int32_t E[10];
     {
       /* Bi (op bit 6) or this signature's Ai: the row offset by arithmetic,
@@ -1098,6 +1113,51 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
     }
 
+#if FD_QUAD_V2
+    /* C = V (.) rot(V): lane q forms t_q t_{q+1}, so C = [T, Y, Z, X] and
+       only g needs a quad move (X = t3 t0 takes its operands in the other
+       order than the reference's t0 t3: the same exact column sums, as no
+       operand pre-scale wraps at the DSM's limb sizes, tests/test_fe_host.py);
+       limbs come out biased, the bias folded into f's constant below */
+    fe Cb;
+    fd_fe_qperm<FD_QP(1,2,3,0)>( g, vt );
+    fd_fe_mul_b( Cb, vt, g );
+
+    /* f = a C + b C' (C' from lane 3,3,2,1 by a DPP-folded v_and):
+       q0 D: X, A: T; q1 X+Y; q2 Z; q3 D: Y, A: Y-X.  g: E on an add, f on a
+       doubling (q2: 2Z).  h = f g = [S, P, Q, R] */
+    uint32_t const mA = fd_ok_mask( kd, FD_Q2_MA ), sA = fd_ok_mask( kd, FD_Q2_SA );
+    uint32_t const mBv = (uint32_t)fd_opaque( (int32_t)fd_ok_mask( kd, FD_Q2_MB ) );
+    uint32_t const kfe = kd & 0xFF000001u;                                     /* sA - (a+b) 2^25 */
+    uint32_t const kfo = (uint32_t)((int32_t)(kd & 0xFF000000u) >> 1) + (kd & 1u);  /* sA - (a+b) 2^24 */
+    uint32_t const gs = fd_ok_bits( kd, FD_Q2_GS, 1 );
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      uint32_t const p = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,2,1)>( Cb.v[k] ) & mBv) );
+      uint32_t const fk = fd_andxor( (uint32_t)Cb.v[k], mA, sA ) + p + ((k & 1) ? kfo : kfe);
+      f.v[k] = (int32_t)fk;
+      g.v[k] = (int32_t)fd_sel( madd, (uint32_t)E[k], fk << gs );
+    }
+    fe h; fd_fe_mul_b( h, f, g );
+
+    /* V' = cP P + cQ Q + cR R + cS S from h = [S, P, Q, R] (the masks of
+       fd_op_kind_bits per output lane), the biases of h folded into K */
+    uint32_t const mP = fd_ok_mask( kd, FD_Q2_MP ), mQ = fd_ok_mask( kd, FD_Q2_MQ ), qs = madd & 1u;
+    uint32_t const mR = fd_ok_mask( kd, FD_Q2_MR ), sR = fd_ok_mask( kd, FD_Q2_SR );
+    uint32_t const mS = fd_ok_mask( kd, FD_Q2_MS ), sS = fd_ok_mask( kd, FD_Q2_SS );
+    uint32_t const cadd = fd_ok_bits( kd, FD_Q2_CADD, 2 ), sc = fd_ok_bits( kd, FD_Q2_SUMC, 8 );
+    uint32_t const Ke = (sc << 25) + cadd, Ko = (sc << 24) + cadd;
+    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
+    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( h.v[k] ) & mPv) );
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( h.v[k] ) & mQv) );
+      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( h.v[k] ) & mRv) );
+      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( h.v[k] ) & mSv) );
+      vt.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + ((k & 1) ? Ko : Ke));
+    }
+#else
     fe C;
     fd_fe_qperm<FD_QP(2,1,0,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
     FD_QMUL( C, f, g );
@@ -1150,6 +1210,7 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     for( int k=0; k<10; k++ )
       vt.v[k] = (int32_t)(((uint32_t)P.v[k] & mP) + (((uint32_t)Q.v[k] & mQ) << qs)
                           + (((uint32_t)R.v[k] & mR) ^ sR) + (((uint32_t)S.v[k] & mS) ^ sS) + cadd);
+#endif
 #endif
   }
 

@@ -87,6 +87,64 @@ FD_DEV uint64_t fd_op_kind_word( uint32_t q ) {
   return (uint64_t)fd_op_kind_bits( q, 0, 0 ) | ((uint64_t)fd_op_kind_bits( q, 1, 0 ) << 16)
        | ((uint64_t)fd_op_kind_bits( q, 1, 1 ) << 32);
 }
+/* The quad DSM's step (fd_quad_body), per lane and op kind, as one
+   32-bit word per kind (three per lane, selected by the op byte's bits 7
+   and 5).  Lane layout of the step:
+     C = V (.) rot(V): lane q multiplies its p1p1 component t_q by t_{q+1},
+       so C = [T, Y, Z, X] (only the first operand pair needs a DPP move);
+     f = a C + b C', C' the partner lane's C (quad_perm 3,3,2,1):
+       q0 D: X (0,1), A: T (1,0); q1 X+Y (1,1); q2 Z (1,0);
+       q3 D: Y (0,1), A: Y-X (-1,1);
+     g = E (add) or f (D; q2: 2f), so h = [S, P, Q, R]:
+       D [X^2, (X+Y)^2, 2Z^2, Y^2], A [TT, PP, ZZ, MM];
+     t_q = the output mix of fd_op_kind_bits (mP..sS, cadd) over those
+       source lanes.
+   C and h arrive with each limb's carry bias in (fd_fe_limbs_t<1>), so
+   the two adds that already take a per-lane constant fold the biases out:
+   f's constant kf = sA - (a+b) bias, the mix's K = cadd - (sum of its
+   coefficients, Q counted twice on an add) bias, bias = 2^25 / 2^24 for
+   even / odd limbs.
+     bit  0     sA (a < 0, as 0/1; also the mask)   bits 4-5  idx (table entry lane)
+     bit  1     mA (a != 0)                          bits 6-13 mP mQ mR sR mS sS, cadd (2)
+     bit  2     mB (b != 0)                          bits 16-23 (-sum c) mod 256
+     bit  3     gs (g = 2f)                          bits 24-31 (-2(a+b)) mod 256
+   so kf_even = w & 0xFF000001 and K_even/odd = ((-sum c) << 25/24) + cadd. */
+#define FD_Q2_SA   0
+#define FD_Q2_MA   1
+#define FD_Q2_MB   2
+#define FD_Q2_GS   3
+#define FD_Q2_IDX  4
+#define FD_Q2_MP   6
+#define FD_Q2_MQ   7
+#define FD_Q2_MR   8
+#define FD_Q2_SR   9
+#define FD_Q2_MS   10
+#define FD_Q2_SS   11
+#define FD_Q2_CADD 12
+#define FD_Q2_SUMC 16
+#define FD_Q2_NF   24
+FD_DEV uint32_t fd_q2_kind_bits( uint32_t q, int add, int neg ) {
+  uint32_t q0 = q == 0u, q1 = q == 1u, q2 = q == 2u, q3 = q == 3u;
+  uint32_t a = add ? 1u : 0u, na = 1u - a, pos = a & (neg ? 0u : 1u), npos = 1u - pos;
+  /* f = fa C + fb C' */
+  int fa = q0 ? (int)a : q1 ? 1 : q2 ? 1 : (add ? -1 : 0);
+  int fb = q0 ? (int)na : q1 ? 1 : q2 ? 0 : 1;
+  uint32_t idx = q0 ? 3u : q1 ? (neg ? 1u : 2u) : q2 ? 0u : (neg ? 2u : 1u);
+  /* the output mix (the same per output lane as fd_op_kind_bits) */
+  uint32_t mP = q0 | (q1 & a), mQ = q3 | (q2 & a), mR = q0 | q1 | na, mS = 1u - ((q0 | q1) & a);
+  uint32_t sR = q0 | (q3 & na), sS = (q0 & na) | (q2 & npos) | (q3 & pos);
+  int sumc = (int)mP + (int)mQ*(add ? 2 : 1) + (int)mR*(sR ? -1 : 1) + (int)mS*(sS ? -1 : 1);
+  return (uint32_t)(fa < 0)                          << FD_Q2_SA
+       | (uint32_t)(fa != 0)                         << FD_Q2_MA
+       | (uint32_t)(fb != 0)                         << FD_Q2_MB
+       | ( q2 & na )                                 << FD_Q2_GS
+       | idx                                         << FD_Q2_IDX
+       | mP << FD_Q2_MP | mQ << FD_Q2_MQ | mR << FD_Q2_MR | sR << FD_Q2_SR | mS << FD_Q2_MS | sS << FD_Q2_SS
+       | ( sR + sS )                                 << FD_Q2_CADD
+       | ((uint32_t)(-sumc) & 0xFFu)                 << FD_Q2_SUMC
+       | ((uint32_t)(-2*(fa + fb)) & 0xFFu)          << FD_Q2_NF;
+}
+
 /* this lane's field for op: kind 0/1/2 = bit 7 + bit 5 */
 FD_DEV uint32_t fd_op_kind( uint64_t kw, int op ) {
   uint32_t k = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);

@@ -150,15 +150,17 @@ struct fd_verify_tile {
   std::vector<int>          out;
   unsigned long             diag[ FD_VERIFY_TILE_DIAG_CNT ];
   /* feeder mode (fd_verify_tile_new_multi): batches are built in host
-     buffers owned per engine (registered with it, so its feeder DMAs them
-     in place) and pushed round robin to the engines' feeders */
+     buffers of one pool shared by the engines (one region registered with
+     every engine, so any engine's feeder DMAs any batch in place) and each
+     is pushed, when it closes, to the engine with the fewest signatures on
+     its device (fd_vt_pick_engine) */
   int                       multi, gpu_cnt, next;
   fd_ed25519_gpu_t *        gpus   [ FD_VERIFY_TILE_GPU_MAX ];
   fd_ed25519_gpu_feeder_t * feeders[ FD_VERIFY_TILE_GPU_MAX ];
-  uint8_t *                 region [ FD_VERIFY_TILE_GPU_MAX ];   /* one allocation per engine */
+  uint8_t *                 region;                            /* the shared batch buffers */
   int                       reg_ok [ FD_VERIFY_TILE_GPU_MAX ];
+  int                       cap    [ FD_VERIFY_TILE_GPU_MAX ];   /* batches an engine may hold: 2 x its depth */
   unsigned long             region_sz;
-  std::vector<fd_vt_batch *> epool [ FD_VERIFY_TILE_GPU_MAX ];   /* free batches per engine */
   std::vector<fd_vt_batch *> all;
   /* in-place mode (fd_verify_tile_new_inplace): frags are referenced where
      they lie in the caller's registered region and DMA'd from there; a
@@ -242,9 +244,29 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
   fd_vt_prof[7]++;
 #endif
   b->txns.clear(); b->ticket = 0;
-  if( t->multi ) t->epool[ b->eng ].push_back( b );
-  else           t->pool.push_back( b );
+  t->pool.push_back( b );
   return 1;
+}
+
+/* Multi-engine mode: the engine a closed batch goes to -- of the engines
+   running fewer than their cap of unfinished batches, the one with the
+   fewest signatures still on its device (pushed, not yet finished: a slower
+   device holds more), ties in round-robin order from t->next (round-4
+   verdict: a static round robin lets the slowest GPU set the tile's rate).
+   The buffers are shared, so a batch freed by an in-order publish can go
+   to whichever engine has drained.  -1: every engine is at its cap. */
+static int fd_vt_pick_engine( fd_verify_tile_t * t ) {
+  unsigned long out[ FD_VERIFY_TILE_GPU_MAX ] = { 0 };
+  int held[ FD_VERIFY_TILE_GPU_MAX ] = { 0 };
+  for( fd_vt_batch const * b : t->inflight )
+    if( !__atomic_load_n( &b->job.state, __ATOMIC_ACQUIRE ) ) { held[ b->eng ]++; out[ b->eng ] += b->nsig; }
+  int best = -1;
+  for( int k=0; k<t->gpu_cnt; k++ ) {
+    int e = (t->next + k) % t->gpu_cnt;
+    if( held[e] >= t->cap[e] ) continue;
+    if( best < 0 || out[e] < out[best] ) best = e;
+  }
+  return best;
 }
 
 /* publish finished batches in order; with block, at least the oldest */
@@ -260,6 +282,21 @@ static int fd_vt_drain( fd_verify_tile_t * t, int block ) {
 }
 
 static int fd_vt_drain( fd_verify_tile_t * t, int block );
+
+/* multi-engine mode: wait until some engine finishes (or fails) one of its
+   unfinished batches, bounded by the slowest engine's timeout */
+static int fd_vt_wait_any( fd_verify_tile_t * t ) {
+  long to = 0;
+  for( int e=0; e<t->gpu_cnt; e++ ) { long x = fd_ed25519_gpu_timeout( t->gpus[e] ); if( x < 0 ) { to = -1; break; } if( x > to ) to = x; }
+  unsigned long t0 = fd_vt_now();
+  for(;;) {
+    if( fd_vt_pick_engine( t ) >= 0 ) return 0;   /* an engine finished a batch: it is below its cap */
+    unsigned long dt = fd_vt_now() - t0;
+    if( to >= 0 && dt > (unsigned long)to ) return FD_ED25519_ERR_GPU;
+    if( dt < 200000UL ) _mm_pause();
+    else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
+  }
+}
 
 static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
@@ -278,11 +315,23 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
       if( err ) return err;
     }
   } else if( t->multi ) {
+    for(;;) {
+      /* an engine below its cap; else wait for ANY engine to finish a
+         batch (not for the oldest: that one may sit on the slowest device
+         while a faster one is free), publishing what is in order */
+      b->eng = fd_vt_pick_engine( t );
+      if( b->eng >= 0 ) break;
+      if( t->inflight.empty() ) return FD_ED25519_ERR_GPU;
+      t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
+      int err = fd_vt_wait_any( t );
+      if( !err ) err = fd_vt_drain( t, 0 );
+      if( err ) return err;
+    }
     memset( &b->job, 0, sizeof(b->job) );
     b->job.n = b->nsig; b->job.blob = b->blob; b->job.blob_sz = b->alen ? b->alen : b->used; b->job.desc = b->desc; b->job.out = b->codes;
     if( b->alen ) { b->job.blob2 = b->blob2; b->job.blob2_sz = b->used - b->alen; }
     if( fd_ed25519_gpu_feeder_push( t->feeders[ b->eng ], &b->job ) ) return FD_ED25519_ERR_GPU;
-    t->next = (b->eng + 1) % t->gpu_cnt;   /* the next batch goes to the next engine */
+    t->next = (b->eng + 1) % t->gpu_cnt;   /* ties go round robin */
   } else {
     int err = fd_ed25519_gpu_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
     if( err ) return FD_ED25519_ERR_GPU;
@@ -320,12 +369,7 @@ static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsig
   }
   while( !t->open ) {
     fd_vt_batch * nb = NULL;
-    if( t->multi ) {   /* a free batch of the next engine in round-robin order */
-      for( int k=0; k<t->gpu_cnt && !nb; k++ ) {
-        int e = (t->next + k) % t->gpu_cnt;
-        if( !t->epool[e].empty() ) { nb = t->epool[e].back(); t->epool[e].pop_back(); }
-      }
-    } else if( !t->pool.empty() ) { nb = t->pool.back(); t->pool.pop_back(); }
+    if( !t->pool.empty() ) { nb = t->pool.back(); t->pool.pop_back(); }   /* the engine is chosen when it closes */
     if( nb ) {
       nb->blob = (uint8_t *)f; nb->used = 0; nb->nsig = 0; nb->ticket = 0; nb->alen = 0; nb->blob2 = NULL;
       t->open = nb;
@@ -347,15 +391,13 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
   }
   while( !t->open ) {
     if( t->multi ) {
-      /* a free batch of the next engine in round-robin order */
-      for( int k=0; k<t->gpu_cnt && !t->open; k++ ) {
-        int e = (t->next + k) % t->gpu_cnt;
-        if( t->epool[e].empty() ) continue;
-        fd_vt_batch * b = t->epool[e].back(); t->epool[e].pop_back();
+      /* a free shared buffer (the engine is chosen when the batch closes) */
+      if( !t->pool.empty() ) {
+        fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
         b->used = 0; b->nsig = 0; b->ticket = 0;
         t->open = b;
+        break;
       }
-      if( t->open ) break;
     } else {
       void * blob; fd_ed25519_gpu_desc_t * desc;
       if( !fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ) {
@@ -399,10 +441,11 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
 
 /* Feeder mode: one tile driving gpu_cnt engines through their per-GPU
    feeders (fd_ed25519_gpu_feeder_*: a thread per engine, pinned to the
-   GPU's NUMA node, keeping that engine's whole ring in flight).  Each
-   engine owns 2 x depth batch buffers in one host allocation registered
-   with it; batches go to the engines round robin and are published in
-   arrival order, as with one engine. */
+   GPU's NUMA node, keeping that engine's whole ring in flight).  The
+   batch buffers (4 x depth per engine) sit in one host allocation
+   registered with every engine; a batch goes, when it closes, to the
+   engine with the fewest signatures on its device, and batches are
+   published in arrival order, as with one engine. */
 static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsigned long gpu_cnt,
                                            fd_verify_tile_cfg_t const * cfg,
                                            fd_verify_tile_publish_fn publish, void * ctx,
@@ -432,15 +475,34 @@ static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsi
   unsigned long blob_room = t->inplace ? 0UL : (maxb + 64UL + 63UL) & ~63UL;
   unsigned long per = blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL)
                     + ((c.batch_sigs * sizeof(int) + 63UL) & ~63UL);
-  int ok = 1;
-  for( unsigned long e=0; e<gpu_cnt && ok; e++ ) {
+  /* 4 x depth buffers per engine, at most 2 x depth of them unfinished on
+     it: finished batches wait for their in-order publish behind an older
+     batch on a slower engine, and the spare buffers keep the faster
+     engines fed meanwhile */
+  int ok = 1, nb = 0;
+  for( unsigned long e=0; e<gpu_cnt; e++ ) {
     t->gpus[e] = gpus[e];
-    int nb = 2 * fd_ed25519_gpu_depth( gpus[e] );
-    t->region_sz = per * (unsigned long)nb;
-    void * r = NULL;
-    if( posix_memalign( &r, 4096UL, t->region_sz ) ) { ok = 0; break; }
-    t->region[e] = (uint8_t *)r;
+    t->cap[e] = 2 * fd_ed25519_gpu_depth( gpus[e] );
+    nb += 2 * t->cap[e];
+  }
+  t->region_sz = per * (unsigned long)nb;
+  void * r = NULL;
+  if( posix_memalign( &r, 4096UL, t->region_sz ) ) ok = 0;
+  else {
+    t->region = (uint8_t *)r;
     memset( r, 0, t->region_sz );
+    for( int k=0; k<nb; k++ ) {
+      fd_vt_batch * b = new fd_vt_batch();
+      uint8_t * p = t->region + per * (unsigned long)k;
+      b->blob  = p;
+      b->desc  = (fd_ed25519_gpu_desc_t *)(p + blob_room);
+      b->codes = (int *)(p + blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL));
+      b->eng = 0; b->ticket = 0; b->used = 0; b->nsig = 0;
+      t->pool.push_back( b );
+      t->all.push_back( b );
+    }
+  }
+  for( unsigned long e=0; e<gpu_cnt && ok; e++ ) {
     /* registered: the feeder DMAs each batch in place (no staging copy);
        without it (no GPU-visible mapping) the feeder copies it into a slot.
        In place it is the input region that every engine DMAs from, and a
@@ -448,17 +510,7 @@ static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsi
     if( t->inplace ) {
       t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], (void *)ip_region, ip_region_sz );
       if( !t->reg_ok[e] ) ok = 0;
-    } else t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], r, t->region_sz );
-    for( int k=0; k<nb; k++ ) {
-      fd_vt_batch * b = new fd_vt_batch();
-      uint8_t * p = t->region[e] + per * (unsigned long)k;
-      b->blob  = p;
-      b->desc  = (fd_ed25519_gpu_desc_t *)(p + blob_room);
-      b->codes = (int *)(p + blob_room + ((c.batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL) & ~63UL));
-      b->eng = (int)e; b->ticket = 0; b->used = 0; b->nsig = 0;
-      t->epool[e].push_back( b );
-      t->all.push_back( b );
-    }
+    } else t->reg_ok[e] = !fd_ed25519_gpu_register( gpus[e], t->region, t->region_sz );
     t->feeders[e] = fd_ed25519_gpu_feeder_new( gpus[e], 1 );
     if( !t->feeders[e] ) ok = 0;
   }
@@ -534,10 +586,10 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
     for( int e=0; e<t->gpu_cnt; e++ ) {
       if( t->reg_ok[e] ) {
         if( t->inplace ) fd_ed25519_gpu_unregister( t->gpus[e], (void *)t->ip_region );
-        else if( t->region[e] ) fd_ed25519_gpu_unregister( t->gpus[e], t->region[e] );
+        else if( t->region ) fd_ed25519_gpu_unregister( t->gpus[e], t->region );
       }
-      free( t->region[e] );
     }
+    free( t->region );
     for( fd_vt_batch * b : t->all ) delete b;
     fd_vt_tcache_delete( t->tc );
     delete t;

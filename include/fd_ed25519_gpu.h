@@ -468,14 +468,20 @@ int fd_ed25519_gpu_feeder_synth( fd_ed25519_gpu_feeder_t *     feeder,
 
 /* ---- Multi-device --------------------------------
 
-   Several engines fed by one host: a batch is sharded into contiguous
-   signature ranges, one per engine (ndev entries of devices[], repeats
-   allowed), each cut into chunks that fit the engine; every engine has
-   its own feeder thread (pinned to its GPU's NUMA node) that keeps its
-   ring full with its chunks, each receiving only the blob bytes it
-   references, and the codes land in out[] in index order.  No
-   collective: the path has no exchange step.  Same codes and error
-   behaviour as fd_ed25519_gpu_verify_packed. */
+   Several engines fed by one host (ndev entries of devices[], repeats
+   allowed): a batch is cut into chunks of contiguous signatures (guided:
+   remaining / (2 ndev), at least chunk_min, at most what every engine
+   takes) dealt dynamically -- the next chunk to the engine with the fewest
+   signatures outstanding that has room (ring depth + 1 chunks), so a
+   slower device takes fewer chunks.  Every engine has its own feeder
+   thread (pinned to its GPU's NUMA node) that keeps its ring full, each
+   chunk moving only the blob bytes it references; the codes land in out[]
+   at their indices.  No collective: the path has no exchange step.  Same
+   codes and error behaviour as fd_ed25519_gpu_verify_packed; a chunk whose
+   engine fails with ERR_GPU is run once more on another engine (which
+   then takes no more chunks), and the whole call is bounded by the multi
+   timeout (default 60 s): past it no further chunk is dealt, the chunks
+   already dealt are collected, and the call returns ERR_GPU. */
 
 typedef struct fd_ed25519_gpu_multi fd_ed25519_gpu_multi_t;
 
@@ -487,6 +493,13 @@ fd_ed25519_gpu_multi_t *
 fd_ed25519_gpu_multi_new_ex( int const * devices, int ndev, unsigned long max_sigs, unsigned long max_blob, int depth );
 
 fd_ed25519_gpu_feeder_t * fd_ed25519_gpu_multi_feeder( fd_ed25519_gpu_multi_t * multi, int idx );
+
+/* Dispatch knobs: the guided chunks' floor (default 65,536 signatures) and
+   the bound on one multi call (ns, < 0 none; default 60 s). */
+int fd_ed25519_gpu_multi_set_chunk_min( fd_ed25519_gpu_multi_t * multi, unsigned long sigs );
+int fd_ed25519_gpu_multi_set_timeout  ( fd_ed25519_gpu_multi_t * multi, long timeout_ns );
+/* Signatures engine idx ran in the last multi call (the dynamic split). */
+unsigned long fd_ed25519_gpu_multi_dealt( fd_ed25519_gpu_multi_t const * multi, int idx );
 
 void               fd_ed25519_gpu_multi_delete( fd_ed25519_gpu_multi_t * multi );
 int                fd_ed25519_gpu_multi_cnt   ( fd_ed25519_gpu_multi_t const * multi );

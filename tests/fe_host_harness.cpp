@@ -5,6 +5,7 @@
 // Test infrastructure only.
 #include "fd_ed25519_gpu_fe.h"
 #include "fd_ed25519_gpu_wnaf.h"
+#include "fd_ed25519_tables.h"
 
 extern "C" {
 /* op stream of n (S, k) scalar pairs (32 bytes each, little endian) into
@@ -73,6 +74,150 @@ void h_fe_invert( int32_t * h, int32_t const * f, unsigned long n ) {
     for( int k=0; k<10; k++ ) a.v[k] = f[10*i+k];
     fd_fe_invert( c, a );
     for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
+
+/* The quad DSM (fd_quad_body in fd_ed25519_gpu_kernels.hip) restated with
+   the four lanes of a signature's quad as an array: the DPP quad moves
+   become index permutations, every per-lane mask and constant comes from
+   the same fd_q2_kind_bits / fd_fe_mul_b the kernel uses.  [a]A + [b]B
+   as p2 limbs (X, Y, Z: 30 int32), for tests/test_quad_model.py to hold
+   against the reference's fd_ed25519_ge_double_scalarmult_vartime limb for
+   limb.  maxlimb (optional) returns the largest |limb| of any product
+   operand in the main loop (the no-wrap bound of the commuted product). */
+typedef fd_gpu_fe_t fe;
+static void m_perm( fe (&o)[4], fe const (&x)[4], int a, int b, int c, int d ) {
+  fe t[4] = { x[a], x[b], x[c], x[d] };
+  for( int q=0; q<4; q++ ) o[q] = t[q];
+}
+static uint32_t m_qterm( uint32_t x, uint32_t m, uint32_t s ) { return ((x & m) ^ s) - s; }
+static void m_subadd12( fe (&x)[4] ) {   /* [a, b-c, b+c, d] */
+  fe p[4]; m_perm( p, x, 0, 2, 1, 3 );
+  for( int q=0; q<4; q++ ) {
+    uint32_t m12 = (q==1 || q==2) ? ~0u : 0u, s1 = q==1 ? ~0u : 0u;
+    for( int k=0; k<10; k++ ) x[q].v[k] = (int32_t)((uint32_t)x[q].v[k] + m_qterm( (uint32_t)p[q].v[k], m12, s1 ));
+  }
+}
+static void m_submix( fe (&x)[4] ) {     /* [c-b, c+b, 2a-d, 2a+d] */
+  fe u[4], w[4]; m_perm( u, x, 2, 2, 0, 0 ); m_perm( w, x, 1, 1, 3, 3 );
+  for( int q=0; q<4; q++ ) {
+    uint32_t sh = (uint32_t)q >> 1, se = (q & 1) ? 0u : ~0u;
+    for( int k=0; k<10; k++ ) x[q].v[k] = (int32_t)(((uint32_t)u[q].v[k] << sh) + m_qterm( (uint32_t)w[q].v[k], ~0u, se ));
+  }
+}
+static void m_dblmix( fe (&x)[4] ) {     /* [a-b-c, b+c, b-c, d-b+c] */
+  fe b[4], c[4]; m_perm( b, x, 1, 1, 1, 1 ); m_perm( c, x, 2, 2, 2, 2 );
+  for( int q=0; q<4; q++ ) {
+    uint32_t m03 = (q==0 || q==3) ? ~0u : 0u, s02 = (q==0 || q==2) ? ~0u : 0u;
+    for( int k=0; k<10; k++ )
+      x[q].v[k] = (int32_t)(((uint32_t)x[q].v[k] & m03) + m_qterm( (uint32_t)b[q].v[k], ~0u, m03 ) + m_qterm( (uint32_t)c[q].v[k], ~0u, s02 ));
+  }
+}
+static void m_mul4( fe (&h)[4], fe const (&f)[4], fe const (&g)[4] ) { for( int q=0; q<4; q++ ) fd_fe_mul( h[q], f[q], g[q] ); }
+static int32_t m_abs( int32_t x ) { return x < 0 ? -x : x; }
+
+int h_quad_dsm( int32_t * out, int32_t const * A, uint8_t const * ops, int start, int32_t * maxlimb ) {
+  fe one; fd_fe_set( one, 1 );
+  fe r[4], vu[4], vt[4], f[4], g[4], d111[4];
+  int const comp[4] = { 20, 10, 0, 30 };            /* [Z, Y, X, T] */
+  for( int q=0; q<4; q++ ) {
+    for( int k=0; k<10; k++ ) r[q].v[k] = A[comp[q]+k];
+    d111[q] = q==3 ? FD_GPU_D2 : one;
+  }
+  fe tab[8][4];
+  /* Ai = {A, 3A, ..., 15A} cached, as the kernel's prologue */
+  m_mul4( vu, r, d111 ); m_subadd12( vu );
+  for( int q=0; q<4; q++ ) tab[0][q] = vu[q];
+  {
+    fe a[4], b[4]; m_perm( a, r, 2, 1, 2, 0 ); m_perm( b, r, 1, 1, 1, 1 );
+    for( int q=0; q<4; q++ ) for( int k=0; k<10; k++ ) {
+      f[q].v[k] = (int32_t)((uint32_t)a[q].v[k] + ((uint32_t)b[q].v[k] & (q==0 ? ~0u : 0u)));
+      g[q].v[k] = (int32_t)((uint32_t)f[q].v[k] << (q==3 ? 1 : 0));
+    }
+    m_mul4( vt, f, g ); m_dblmix( vt );
+  }
+  m_perm( f, vt, 3, 2, 3, 1 ); m_perm( g, vt, 2, 1, 0, 0 );
+  m_mul4( r, f, g ); m_subadd12( r );
+  for( int e=0; e<7; e++ ) {
+    m_mul4( vt, r, vu ); m_submix( vt );
+    m_perm( f, vt, 2, 3, 2, 1 ); m_perm( g, vt, 3, 1, 0, 0 );
+    m_mul4( vt, f, g );
+    m_mul4( vu, vt, d111 ); m_subadd12( vu );
+    for( int q=0; q<4; q++ ) tab[e+1][q] = vu[q];
+  }
+  fe bi[8][4];
+  for( int e=0; e<8; e++ ) for( int q=0; q<4; q++ ) bi[e][q] = FD_GPU_BI_PRECOMP[e].l[q];
+
+  /* main loop (FD_QUAD_V2) */
+  uint32_t kw[3][4];
+  for( int q=0; q<4; q++ ) { kw[0][q] = fd_q2_kind_bits( q, 0, 0 ); kw[1][q] = fd_q2_kind_bits( q, 1, 0 ); kw[2][q] = fd_q2_kind_bits( q, 1, 1 ); }
+  for( int q=0; q<4; q++ ) fd_fe_set( vt[q], q ? 1 : 0 );
+  int32_t mx = 0;
+  for( int t=start; t<FD_OPS_MAX; t++ ) {
+    int op = ops[t];
+    int kind = (op >> 7) ? 1 + ((op >> 5) & 1) : 0;
+    fe Cb[4], h[4], E[4];
+    uint32_t kd[4];
+    for( int q=0; q<4; q++ ) {
+      kd[q] = kw[kind][q];
+      uint32_t idx = fd_ok_bits( kd[q], FD_Q2_IDX, 2 );
+      E[q] = ((op >> 6) & 1) ? bi[op & 7][idx] : tab[op & 7][idx];
+    }
+    m_perm( g, vt, 1, 2, 3, 0 );
+    for( int q=0; q<4; q++ ) {
+      for( int k=0; k<10; k++ ) { mx = m_abs( vt[q].v[k] ) > mx ? m_abs( vt[q].v[k] ) : mx; }
+      fd_fe_mul_b( Cb[q], vt[q], g[q] );
+    }
+    fe Cp[4]; m_perm( Cp, Cb, 3, 3, 2, 1 );
+    for( int q=0; q<4; q++ ) {
+      uint32_t w = kd[q];
+      uint32_t mA = fd_ok_mask( w, FD_Q2_MA ), sA = fd_ok_mask( w, FD_Q2_SA ), mB = fd_ok_mask( w, FD_Q2_MB );
+      uint32_t kfe = w & 0xFF000001u, kfo = (uint32_t)((int32_t)(w & 0xFF000000u) >> 1) + (w & 1u);
+      uint32_t gs = fd_ok_bits( w, FD_Q2_GS, 1 ), madd = kind ? ~0u : 0u;
+      for( int k=0; k<10; k++ ) {
+        uint32_t fk = (((uint32_t)Cb[q].v[k] & mA) ^ sA) + ((uint32_t)Cp[q].v[k] & mB) + ((k & 1) ? kfo : kfe);
+        f[q].v[k] = (int32_t)fk;
+        g[q].v[k] = (int32_t)fd_sel( madd, (uint32_t)E[q].v[k], fk << gs );
+        mx = m_abs( f[q].v[k] ) > mx ? m_abs( f[q].v[k] ) : mx;
+        mx = m_abs( g[q].v[k] ) > mx ? m_abs( g[q].v[k] ) : mx;
+      }
+      fd_fe_mul_b( h[q], f[q], g[q] );
+    }
+    for( int q=0; q<4; q++ ) {
+      uint32_t w = kd[q];
+      uint32_t mP = fd_ok_mask( w, FD_Q2_MP ), mQ = fd_ok_mask( w, FD_Q2_MQ ), qs = kind ? 1u : 0u;
+      uint32_t mR = fd_ok_mask( w, FD_Q2_MR ), sR = fd_ok_mask( w, FD_Q2_SR );
+      uint32_t mS = fd_ok_mask( w, FD_Q2_MS ), sS = fd_ok_mask( w, FD_Q2_SS );
+      uint32_t cadd = fd_ok_bits( w, FD_Q2_CADD, 2 ), sc = fd_ok_bits( w, FD_Q2_SUMC, 8 );
+      uint32_t Ke = (sc << 25) + cadd, Ko = (sc << 24) + cadd;
+      for( int k=0; k<10; k++ )
+        vt[q].v[k] = (int32_t)(((uint32_t)h[1].v[k] & mP) + (((uint32_t)h[2].v[k] & mQ) << qs)
+                               + (((uint32_t)h[3].v[k] & mR) ^ sR) + (((uint32_t)h[0].v[k] & mS) ^ sS) + ((k & 1) ? Ko : Ke));
+    }
+  }
+  /* p1p1 -> p2: X = t0 t3, Y = t1 t2, Z = t2 t3 */
+  m_perm( f, vt, 0, 1, 2, 0 ); m_perm( g, vt, 3, 2, 3, 1 );
+  fe P2[4]; m_mul4( P2, f, g );
+  for( int c=0; c<3; c++ ) for( int k=0; k<10; k++ ) out[10*c+k] = P2[c].v[k];
+  if( maxlimb ) *maxlimb = mx;
+  return 0;
+}
+/* the quad's commuted product (C's lane 3): g*f, for the no-wrap range test */
+void h_fe_mul_swapped( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, b, c;
+    for( int k=0; k<10; k++ ) { a.v[k] = f[10*i+k]; b.v[k] = g[10*i+k]; }
+    fd_fe_mul( c, b, a );
+    for( int k=0; k<10; k++ ) h[10*i+k] = c.v[k];
+  }
+}
+/* fd_fe_mul_b (biased limbs) minus the biases: equals fd_fe_mul */
+void h_fe_mul_b( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
+  for( unsigned long i=0; i<n; i++ ) {
+    fd_gpu_fe_t a, b, c;
+    for( int k=0; k<10; k++ ) { a.v[k] = f[10*i+k]; b.v[k] = g[10*i+k]; }
+    fd_fe_mul_b( c, a, b );
+    for( int k=0; k<10; k++ ) h[10*i+k] = (int32_t)((uint32_t)c.v[k] - ((k & 1) ? (1u<<24) : (1u<<25)));
   }
 }
 }

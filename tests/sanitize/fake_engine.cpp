@@ -11,9 +11,16 @@
    For the feeder (fd_ed25519_gpu_feeder.cpp) it also provides the
    engine's device / timeout accessors, the two HIP calls the feeder makes
    (no GPU: no NUMA node, a no-op set-device), and a "wedged device" switch
-   (fake_engine_wedge): batches submitted while it is on never complete. */
+   (fake_engine_wedge): batches submitted while it is on never complete.
+   For the multi-device dispatch tests it can also model a device's speed
+   (fake_engine_speed: a batch occupies the engine for n x ns_per_sig,
+   batches back to back, and completes only then) and compute codes with
+   a cheap stand-in instead of the restatement (fake_engine_cheap: ERR_SIG
+   when the signature's first byte is odd), so a makespan is the modelled
+   device time, not the CPU verify. */
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <vector>
 #include <mutex>
 #include "fd_ed25519_gpu.h"
@@ -22,9 +29,14 @@
 extern "C" int oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
 
 #define FAKE_DEPTH_MAX 8
-struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket; int staged, polls, wedged; };
+/* engines created from now on start with cheap codes (for tests whose
+   engines are made inside the code under test) */
+static int fake_cheap_default = 0;
+extern "C" void fake_engine_cheap_default( int on ) { fake_cheap_default = on; }
+struct fake_slot { uint8_t * blob; fd_ed25519_gpu_desc_t * desc; int * out; unsigned long n, ticket, done_at; int staged, polls, wedged; };
 struct fd_ed25519_gpu {
-  unsigned long max_sigs, max_blob, next; int depth, wedge, fail_submit; long timeout_ns;
+  unsigned long max_sigs, max_blob, next; int depth, wedge, fail_submit, cheap; long timeout_ns;
+  unsigned long ns_per_sig, busy_until, sigs;
   fake_slot slot[ FAKE_DEPTH_MAX ];
   std::mutex lock;
 };
@@ -34,6 +46,7 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   if( !max_sigs || depth < 1 || depth > FAKE_DEPTH_MAX ) return NULL;
   fd_ed25519_gpu_t * g = new fd_ed25519_gpu_t();
   g->max_sigs = max_sigs; g->max_blob = max_blob; g->depth = depth; g->next = 1; g->timeout_ns = 10000000000L;
+  g->cheap = fake_cheap_default;
   for( int s=0; s<depth; s++ ) {
     g->slot[s].blob = (uint8_t *)malloc( max_blob + 64UL );      /* exactly the engine's pinned blob + pad */
     g->slot[s].desc = (fd_ed25519_gpu_desc_t *)malloc( max_sigs * sizeof(fd_ed25519_gpu_desc_t) );
@@ -53,6 +66,14 @@ extern "C" int  fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { (void)g; r
 extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g ? __atomic_load_n( &g->timeout_ns, __ATOMIC_RELAXED ) : -1; }
 extern "C" int  fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long ns ) { if( !g ) return FD_ED25519_ERR_ARG; __atomic_store_n( &g->timeout_ns, ns, __ATOMIC_RELAXED ); return 0; }
 extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on ) { std::lock_guard<std::mutex> l( g->lock ); g->wedge = on; }
+extern "C" void fake_engine_speed( fd_ed25519_gpu_t * g, unsigned long ns_per_sig ) { std::lock_guard<std::mutex> l( g->lock ); g->ns_per_sig = ns_per_sig; }
+extern "C" void fake_engine_cheap( fd_ed25519_gpu_t * g, int on ) { std::lock_guard<std::mutex> l( g->lock ); g->cheap = on; }
+/* signatures submitted to this engine so far */
+extern "C" unsigned long fake_engine_sigs( fd_ed25519_gpu_t * g ) { std::lock_guard<std::mutex> l( g->lock ); return g->sigs; }
+static unsigned long fake_now( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (unsigned long)ts.tv_sec * 1000000000UL + (unsigned long)ts.tv_nsec;
+}
 /* the next try_submit fails with `code` (a runtime error on a free slot) */
 extern "C" void fake_engine_fail_submit( fd_ed25519_gpu_t * g, int code ) { std::lock_guard<std::mutex> l( g->lock ); g->fail_submit = code; }
 /* the HIP calls of the feeder (C linkage, as hip_runtime_api.h declares them) */
@@ -92,9 +113,15 @@ extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n,
   if( sl->desc != desc ) memcpy( sl->desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   for( unsigned long i=0; i<n; i++ ) {
     fd_ed25519_gpu_desc_t const * d = &sl->desc[i];
-    sl->out[i] = fd_ed25519_desc_ok( d, blob_sz )
-               ? oracle_verify( sl->blob + d->msg_off, d->msg_sz, sl->blob + d->sig_off, sl->blob + d->pub_off )
-               : FD_ED25519_ERR_ARG;
+    sl->out[i] = !fd_ed25519_desc_ok( d, blob_sz ) ? FD_ED25519_ERR_ARG
+               : g->cheap ? ( (sl->blob[ d->sig_off ] & 1) ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS )
+               : oracle_verify( sl->blob + d->msg_off, d->msg_sz, sl->blob + d->sig_off, sl->blob + d->pub_off );
+  }
+  sl->done_at = 0;
+  g->sigs += n;
+  if( g->ns_per_sig ) {   /* the modelled device: batches run back to back */
+    unsigned long now = fake_now(), st = g->busy_until > now ? g->busy_until : now;
+    sl->done_at = g->busy_until = st + n * g->ns_per_sig;
   }
   sl->n = n; sl->staged = 0; sl->polls = 0; sl->wedged = g->wedge;
   sl->ticket = g->next++;
@@ -121,6 +148,19 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
 
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
   if( !g || !ticket ) return FD_ED25519_ERR_ARG;
+  unsigned long wait_until = 0;
+  {
+    std::lock_guard<std::mutex> l( g->lock );
+    for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket == ticket ) wait_until = g->slot[s].done_at;
+  }
+  if( wait_until ) {      /* the modelled device has not finished the batch yet */
+    unsigned long now = fake_now();
+    if( now < wait_until ) {
+      if( !block ) return 0;
+      struct timespec ts = { (long)((wait_until - now) / 1000000000UL), (long)((wait_until - now) % 1000000000UL) };
+      nanosleep( &ts, NULL );
+    }
+  }
   std::lock_guard<std::mutex> l( g->lock );
   for( int s=0; s<g->depth; s++ ) {
     fake_slot * sl = &g->slot[s];

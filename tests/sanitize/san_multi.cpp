@@ -5,19 +5,102 @@
    ~2 % of descriptors outside the blob, chunks larger than an engine's
    ring slot) must come back with exactly the restatement's code per index
    (ERR_ARG for the bad descriptors), twice in a row, and
-   fd_ed25519_codes_to_bitmap must pack the accepts.  Exit 0 and "ok". */
+   fd_ed25519_codes_to_bitmap must pack the accepts.  Then the dynamic
+   dispatch (round-4 verdict item 4) on two engines modelled at unequal
+   speeds (1.0 and 0.88: fake_engine_speed, cheap codes): the call must
+   finish within 5 % of the ideal makespan N / (r1 + r2) with every code
+   right and the faster engine dealt more; with one engine wedged its
+   chunks must move to the other after its timeout (codes still right);
+   and a call bounded by a short multi timeout must return ERR_GPU in
+   about that time.  Exit 0 and "ok". */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <vector>
+#include <algorithm>
 #include "fd_ed25519_gpu.h"
 #include "fd_ed25519_gpu_desc.h"
 
 extern "C" int oracle_verify( void const * msg, unsigned long sz, void const * sig, void const * pub );
+extern "C" void fake_engine_speed( fd_ed25519_gpu_t * g, unsigned long ns_per_sig );
+extern "C" void fake_engine_cheap( fd_ed25519_gpu_t * g, int on );
+extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on );
 
 #define CHECK( c ) do { if( !(c) ) { fprintf( stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c ); exit( 1 ); } } while( 0 )
 
 static unsigned long rnd( unsigned long * s ) { *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17; return *s; }
+
+static double now_s( void ) { struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t ); return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec; }
+
+/* two engines at 1.0 and 0.88 of a 1 us/signature device */
+static void dispatch_tests( void ) {
+  /* the modelled device is slow enough that one chunk's device time dwarfs
+     the host's dispatch work, as a 262,144-signature launch (~4 ms) does a
+     GPU's; ThreadSanitizer slows the host ~10x, so its device is slower */
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#define FD_TSAN 1
+#endif
+#endif
+#ifdef FD_TSAN
+  unsigned long const NS0 = 16000, NS1 = 18182;
+#else
+  unsigned long const NS0 = 4000, NS1 = 4545;
+#endif
+  unsigned long const N = 200000, ITEM = 128;
+  unsigned long blob_sz = N * ITEM, s = 0x9e3779b9UL;
+  std::vector<uint8_t> blob( blob_sz + 64 );
+  for( auto & b : blob ) b = (uint8_t)rnd( &s );
+  std::vector<fd_ed25519_gpu_desc_t> desc( N );
+  std::vector<int> exp( N ), out( N, 99 );
+  for( unsigned long i=0; i<N; i++ ) {
+    fd_ed25519_gpu_desc_t d;
+    d.sig_off = (uint32_t)(i*ITEM); d.pub_off = (uint32_t)(i*ITEM + 64); d.msg_off = (uint32_t)(i*ITEM + 96); d.msg_sz = 32;
+    desc[i] = d;
+    exp[i] = (blob[i*ITEM] & 1) ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
+  }
+  int devs[2] = { 0, 1 };
+  fd_ed25519_gpu_multi_t * m = fd_ed25519_gpu_multi_new_ex( devs, 2, 16384, 16384 * ITEM, 2 );
+  CHECK( m );
+  fd_ed25519_gpu_t * g0 = fd_ed25519_gpu_multi_engine( m, 0 ), * g1 = fd_ed25519_gpu_multi_engine( m, 1 );
+  fake_engine_cheap( g0, 1 ); fake_engine_cheap( g1, 1 );
+  fake_engine_speed( g0, NS0 ); fake_engine_speed( g1, NS1 );
+  CHECK( fd_ed25519_gpu_multi_set_chunk_min( m, 2048 ) == 0 );
+  double ideal = (double)N / ( 1e9 / (double)NS0 + 1e9 / (double)NS1 );
+  double best = 1e9;
+  for( int rep=0; rep<3; rep++ ) {      /* best of three: a loaded CI host may stall a thread once */
+    std::fill( out.begin(), out.end(), 99 );
+    double t0 = now_s();
+    CHECK( fd_ed25519_gpu_multi_verify_packed( m, N, blob.data(), blob_sz, desc.data(), out.data() ) == 0 );
+    double dt = now_s() - t0;
+    CHECK( out == exp );
+    unsigned long d0 = fd_ed25519_gpu_multi_dealt( m, 0 ), d1 = fd_ed25519_gpu_multi_dealt( m, 1 );
+    CHECK( d0 + d1 == N );
+    CHECK( d0 > d1 );
+    fprintf( stderr, "makespan %.1f ms, ideal %.1f ms (%.3f), dealt %lu / %lu\n", dt * 1e3, ideal * 1e3, dt / ideal, d0, d1 );
+    if( dt < best ) best = dt;
+  }
+  CHECK( best <= 1.05 * ideal );
+  /* engine 1 wedged (timeout 50 ms): its chunks fail and run on engine 0 */
+  fd_ed25519_gpu_set_timeout( g1, 50000000L );
+  fake_engine_wedge( g1, 1 );
+  std::fill( out.begin(), out.end(), 99 );
+  CHECK( fd_ed25519_gpu_multi_verify_packed( m, N / 4, blob.data(), blob_sz, desc.data(), out.data() ) == 0 );
+  CHECK( std::equal( out.begin(), out.begin() + N / 4, exp.begin() ) );
+  CHECK( fd_ed25519_gpu_multi_dealt( m, 0 ) == N / 4 && fd_ed25519_gpu_multi_dealt( m, 1 ) == 0 );
+  fake_engine_wedge( g1, 0 );
+  /* the whole call bounded: both engines at 20 us per signature, a 30 ms
+     bound (a call would take ~2 s) */
+  fake_engine_speed( g0, 20000 ); fake_engine_speed( g1, 22727 );
+  CHECK( fd_ed25519_gpu_multi_set_timeout( m, 30000000L ) == 0 );
+  double t0 = now_s();
+  CHECK( fd_ed25519_gpu_multi_verify_packed( m, N, blob.data(), blob_sz, desc.data(), out.data() ) == FD_ED25519_ERR_GPU );
+  double dt = now_s() - t0;
+  fprintf( stderr, "bounded call returned after %.1f ms\n", dt * 1e3 );
+  CHECK( dt < 1.5 );     /* the bound plus the chunks already dealt (3 per engine, 16384 x 22.7 us each) */
+  fd_ed25519_gpu_multi_delete( m );
+}
 
 int main( void ) {
   unsigned long const N = 6000, ITEM = 224;
@@ -55,6 +138,7 @@ int main( void ) {
     acc += out[i] == 0;
   }
   fd_ed25519_gpu_multi_delete( m );
+  dispatch_tests();
   printf( "ok %lu signatures, %lu accepted\n", N, acc );
   return 0;
 }

@@ -10,7 +10,14 @@
         loop on its own thread, the cnc driven from main, BOOT -> RUN,
         every frag consumed, HALT -> flush -> BOOT, same publish stream;
      3. a wedged engine: the tile's blocking drain fails with ERR_GPU after
-        the engine timeout instead of hanging, and delete returns.
+        the engine timeout instead of hanging, and delete returns;
+     4. two engines modelled at unequal speeds (fake_engine_speed, the
+        second 1.25x slower; cheap stand-in codes in every engine of this
+        case, the reference tile's included, so the modelled device time
+        and not the CPU verify sets the pace): the same publish stream as
+        the single-engine tile over the same frags, and the faster engine
+        took at least 1.15x the signatures (fd_vt_pick_engine: each batch to
+        the engine with the fewest unfinished signatures).
    frags file as san_tile.cpp.  Exit 0 and "ok". */
 #include <stdio.h>
 #include <time.h>
@@ -23,6 +30,9 @@
 #define NENG 8
 
 extern "C" void fake_engine_wedge( fd_ed25519_gpu_t * g, int on );
+extern "C" void fake_engine_speed( fd_ed25519_gpu_t * g, unsigned long ns_per_sig );
+extern "C" unsigned long fake_engine_sigs( fd_ed25519_gpu_t * g );
+extern "C" void fake_engine_cheap_default( int on );
 
 static void nap( void ) { struct timespec t = { 0, 200000L }; nanosleep( &t, NULL ); }
 
@@ -131,6 +141,46 @@ int main( int argc, char ** argv ) {
     CHECK( err == FD_ED25519_ERR_GPU );
     fd_verify_tile_delete( t );
     for( int e=0; e<NENG; e++ ) fd_ed25519_gpu_delete( g[e] );
+  }
+  /* 4. unequal engines: a 3x slower second device gets fewer batches */
+  {
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#define FD_TSAN 1
+#endif
+#endif
+#ifdef FD_TSAN
+    unsigned long const ns0 = 80000UL;      /* the modelled device dominates the (10x slower) host */
+#else
+    unsigned long const ns0 = 20000UL;
+#endif
+    /* the stream 16 times over (~150 batches of 128; repeats older than
+       the tcache's 16 tags pass again, for the reference tile as well) */
+    unsigned long const n4 = 16UL * n;
+    std::vector<unsigned char *> fr4( n4 ); std::vector<unsigned long> sz4( n4 );
+    for( unsigned long i=0; i<n4; i++ ) { fr4[i] = fr[i % n]; sz4[i] = sz[i % n]; }
+    fake_engine_cheap_default( 1 );
+    tc_state r4; unsigned long d4r[ FD_VERIFY_TILE_DIAG_CNT ];
+    CHECK( tc_run( fr4.data(), sz4.data(), n4, 128, 8UL << 20, 3, &r4, d4r ) == 0 );
+    fd_ed25519_gpu_t * g[2];
+    for( int e=0; e<2; e++ ) g[e] = fd_ed25519_gpu_new_ex( e, 128, 8UL << 20, 2 );
+    fake_engine_speed( g[0], ns0 ); fake_engine_speed( g[1], ns0 * 5 / 4 );
+    fd_verify_tile_cfg_t cfg = { 128UL, 16UL, 64UL };
+    tc_state s4; memset( &s4, 0, sizeof(s4) ); s4.hash = 1469598103934665603UL;
+    fd_verify_tile_t * t = fd_verify_tile_new_multi( g, 2, &cfg, tc_pub, &s4 );
+    CHECK( t );
+    for( unsigned long i=0; i<n4; i++ ) {
+      CHECK( fd_verify_tile_rx( t, fr4[i], sz4[i], i, i ) == 0 );
+      if( (i % 5) == 0 ) CHECK( fd_verify_tile_service( t, 0 ) == 0 );
+    }
+    CHECK( fd_verify_tile_service( t, 1 ) == 0 );
+    CHECK( s4.pub_cnt == r4.pub_cnt && s4.pub_sz == r4.pub_sz && s4.hash == r4.hash && !s4.bad_order );
+    unsigned long a0 = fake_engine_sigs( g[0] ), a1 = fake_engine_sigs( g[1] );
+    fprintf( stderr, "unequal engines: %lu / %lu signatures\n", a0, a1 );
+    CHECK( a0 * 100 >= a1 * 115 );
+    fd_verify_tile_delete( t );
+    for( int e=0; e<2; e++ ) fd_ed25519_gpu_delete( g[e] );
+    fake_engine_cheap_default( 0 );
   }
   for( auto p : fr ) free( p );
   printf( "ok %u frags, %lu published over %d engines\n", n, st.pub_cnt, NENG );

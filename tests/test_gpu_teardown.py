@@ -68,3 +68,36 @@ def test_exit_with_live_engines(case):
     assert r.stdout.strip().endswith("ok"), r.stdout[-2000:]
     for bad in ("Segmentation fault", "core dumped", "Aborted", "HSA_STATUS_ERROR", "Memory access fault"):
         assert bad not in r.stderr, r.stderr[-4000:]
+
+
+def test_timed_out_calls_do_not_lose_slots():
+    """a per-signature call whose blocking poll times
+    out must orphan its ring slot (reclaimed once the batch drains), not
+    keep it for the engine's lifetime -- otherwise `depth` such stalls leave
+    fd_ed25519_verify with no free slot for good.  Eight calls with a 1 us
+    timeout (each fails with ERR_GPU mid-batch, more than the default
+    engine's 3 slots), then the timeout restored: every later call must
+    return its own code again.  Runs in a child so the default engine it
+    degrades is its own."""
+    code = PRELUDE + """
+import ctypes, time
+L = fa.lib()
+g = L.fd_ed25519_gpu_default()
+assert g
+exp = [fa.verify(b.msg(i), b.sig(i), b.pub(i)) for i in range(16)]
+old = L.fd_ed25519_gpu_timeout(g)
+assert L.fd_ed25519_gpu_set_timeout(g, 1000) == 0
+fails = sum(fa.verify(b.msg(i), b.sig(i), b.pub(i)) == fa.ERR_GPU for i in range(8))
+assert L.fd_ed25519_gpu_set_timeout(g, old) == 0
+time.sleep(0.2)
+got = [fa.verify(b.msg(i), b.sig(i), b.pub(i)) for i in range(16)]
+assert got == exp, (got, exp)
+r, out = fa.verify_batch([b.msg(i) for i in range(64)], [b.sig(i) for i in range(64)], [b.pub(i) for i in range(64)])
+assert [int(x) for x in out[:16]] == exp
+print("fails", fails, flush=True)
+print("ok", flush=True)
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=dict(os.environ), cwd=ROOT)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert r.stdout.strip().endswith("ok"), r.stdout[-2000:]
+    assert "fails 0" not in r.stdout, "the 1 us timeout never fired: the test exercised nothing"
