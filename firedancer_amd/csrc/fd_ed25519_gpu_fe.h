@@ -141,12 +141,38 @@ FD_DEV int64_t fd_mad( int32_t a, int32_t b, int64_t c ) { return fd_opaque64( c
    residuals, the biases removed.  BIASED = 1 leaves each limb's bias in
    (limb k + 2^25 for even k, + 2^24 for odd k: one instruction fewer per
    limb); a consumer that folds the bias into a constant it adds anyway
-   takes these (the quad DSM's operand and output mixes). */
+   takes these (the quad DSM's operand and output mixes).  BIASED = 2
+   (FD_FE_RAW) leaves the residual masks to the consumer as well: limbs
+   0, 2, 4, 6, 8 are the low words of their sums (the limb + 2^25 is that
+   word & (2^26 - 1)), limbs 3, 7, 9 likewise with 2^24 and 2^25 - 1, and
+   limbs 1 and 5 (whose second carry-in c0' / c4', |c| < 2^11, lands after
+   the residual) arrive as limb + 2^24 + FD_FE_RAW_X, in [0, 2^26): a
+   consumer that masks anyway (the quad's DPP-folded v_and, its v_bitop3)
+   takes the 26-bit mask for them and the 2^24 + FD_FE_RAW_X bias. */
+#define FD_FE_RAW    2
+#define FD_FE_RAW_X  4096u
 template<int BIASED>
 FD_DEV void fd_fe_limbs_t( fd_gpu_fe_t & out, int64_t S0, int64_t S1, int64_t S2, int64_t S3, int64_t S4,
                            int64_t S5, int64_t S6, int64_t S7, int64_t S8, int64_t S9 ) {
   int64_t c3 = S3 >> 25, c9 = S9 >> 25;
   uint32_t const m26 = (1u<<26)-1u, m25 = (1u<<25)-1u;
+  if constexpr( BIASED == FD_FE_RAW ) {
+    int64_t  V4  = (int64_t)((uint32_t)S4 & m26) + c3;
+    uint32_t c4b = (uint32_t)(V4 >> 26);
+    int64_t  V0  = (int64_t)((uint32_t)S0 & m26) + c9*19;
+    uint32_t c0b = (uint32_t)(V0 >> 26);
+    out.v[0] = fd_opaque( (int32_t)(uint32_t)V0 );
+    out.v[1] = fd_opaque( (int32_t)(((uint32_t)S1 & m25) + c0b + FD_FE_RAW_X) );
+    out.v[2] = fd_opaque( (int32_t)(uint32_t)S2 );
+    out.v[3] = fd_opaque( (int32_t)(uint32_t)S3 );
+    out.v[4] = fd_opaque( (int32_t)(uint32_t)V4 );
+    out.v[5] = fd_opaque( (int32_t)(((uint32_t)S5 & m25) + c4b + FD_FE_RAW_X) );
+    out.v[6] = fd_opaque( (int32_t)(uint32_t)S6 );
+    out.v[7] = fd_opaque( (int32_t)(uint32_t)S7 );
+    out.v[8] = fd_opaque( (int32_t)(uint32_t)S8 );
+    out.v[9] = fd_opaque( (int32_t)(uint32_t)S9 );
+    return;
+  }
   uint32_t const be = BIASED ? 0u : (1u<<25), bo = BIASED ? 0u : (1u<<24);
   int64_t  V4  = (int64_t)((uint32_t)S4 & m26) + c3;       /* limb 4: second carry */
   uint32_t c4b = (uint32_t)(V4 >> 26);
@@ -374,6 +400,18 @@ FD_DEV void fd_fe_mul( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const
   fd_fe_pre_g( g19, g );
   fd_fe_mul_pre( h, f, f2, g, g19 );
 }
+
+/* the product's limbs as fd_fe_limbs_t<FD_FE_RAW> leaves them */
+FD_DEV void fd_fe_mul_raw( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t const & g ) {
+  int32_t f2[10], g19[10];
+  fd_fe_pre_f( f2, f );
+  fd_fe_pre_g( g19, g );
+  fd_mul_cols c = { f.v, f2, g.v, g19 };
+  fd_fe_chain<fd_mul_cols, FD_FE_RAW>( h, c );
+}
+/* the mask a raw limb k takes and the bias it then carries */
+FD_DEV uint32_t fd_fe_raw_mask( int k ) { return (k & 1) && k != 1 && k != 5 ? (1u<<25)-1u : (1u<<26)-1u; }
+FD_DEV uint32_t fd_fe_raw_bias( int k ) { return !(k & 1) ? (1u<<25) : (k == 1 || k == 5) ? (1u<<24) + FD_FE_RAW_X : (1u<<24); }
 
 /* h + bias (fd_fe_limbs_t<1>): the product with each limb's carry bias
    left in, for consumers that fold it into a constant they add anyway */

@@ -280,8 +280,12 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
   g->quad_max = FD_DSM_QUAD_MAX_DEFAULT;
   g->oct_max  = FD_DSM_OCT_MAX_DEFAULT;
   {
-    char const * od = getenv( "FD_ED25519_GPU_OUT_DIRECT_MAX" );   /* A/B: 0 = always the D2H copy */
-    g->out_direct_max = od ? strtoul( od, NULL, 0 ) : 65536UL;
+    /* the latency path's batches (the ring's 4,096, the per-signature
+       group commits) take the direct write; larger ones the D2H copy,
+       where its ~5 us is noise (tests/test_gpu_host.py
+       checks the direct path at 40,000 too).  A/B: 0 = always the copy */
+    char const * od = getenv( "FD_ED25519_GPU_OUT_DIRECT_MAX" );
+    g->out_direct_max = od ? strtoul( od, NULL, 0 ) : 4096UL;
   }
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );

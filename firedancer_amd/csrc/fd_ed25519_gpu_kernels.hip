@@ -882,6 +882,13 @@ FD_QDEV uint32_t fd_andxor( uint32_t x, uint32_t m, uint32_t s ) { return __buil
 /* ((x & m) ^ s) - s: x, 0, -x or (m = 0, s = ~0) 0, for masks in {0, ~0} */
 FD_QDEV uint32_t fd_qterm( uint32_t x, uint32_t m, uint32_t s ) { return ((x & m) ^ s) - s; }
 
+/* (x ^ s) + y as one v_xad_u32 (LLVM forms xor + add3 otherwise) */
+FD_QDEV uint32_t fd_xad( uint32_t x, uint32_t s, uint32_t y ) {
+  uint32_t r;
+  asm( "v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(s), "v"(y) );
+  return r;
+}
+
 /* SUBADD_12 across the quad: [a, b-c, b+c, d] */
 FD_QDEV void fd_q_subadd12( fe & x, uint32_t m12, uint32_t s1 ) {
   fe p; fd_fe_qperm<FD_QP(0,2,1,3)>( p, x );
@@ -920,9 +927,31 @@ extern "C" hipError_t fd_ed25519_gpu_quad_acc( void * host, int clear ) {
    rows start 4 banks apart, so the step's byte reads of 16 signatures at
    one t hit 16 different banks; 16-byte aligned for ds_write_b128) */
 #define FD_QOPS_ROW (FD_OPS_MAX + 16)
+/* The quad step (FD_QUAD_STEP): 1 round 4's layout; 2 round 5's first
+   (C = V (.) rot V, own/partner operand forms, biased products,
+   fd_q2_kind_bits); 3 (default) the same layout with the per-step decode
+   read from an LDS table (fd_q3_entry), raw product limbs whose residual
+   masks fold into the operand / output masks, and xor-adds in the mix. */
+#ifndef FD_QUAD_STEP
+#define FD_QUAD_STEP 3
+#endif
+#if FD_QUAD_STEP >= 3
+/* op rows from FD_QOPS_BASE on: a stream holds at most 2 x 51 digits
+   (width-5 windows of two scalars below 2^253, fd_ed25519_gpu_wnaf.h), so
+   it starts at FD_OPS_MAX - 256 - 102 = 154 or later; 400-byte rows (100
+   dwords, 36 banks apart) keep the 16 rows' step reads on 16 banks */
+#define FD_QOPS_BASE 144
+#define FD_QOPS_ROWQ 400
+#else
+#define FD_QOPS_BASE 0
+#define FD_QOPS_ROWQ FD_QOPS_ROW
+#endif
 struct fd_quad_lds {
   int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
-  uint8_t ops[FD_QSIGS][FD_QOPS_ROW];   /* signature-major, padded rows */
+  uint8_t ops[FD_QSIGS][FD_QOPS_ROWQ];   /* signature-major, padded rows (from t = FD_QOPS_BASE) */
+#if FD_QUAD_STEP >= 3
+  int32_t dec[3*4*FD_Q3_DW];            /* fd_q3_entry per (op kind, lane) */
+#endif
 };
 FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   int4 * q = (int4 *)p;
@@ -933,9 +962,6 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
 
 #ifndef FD_QUAD_ILP
 #define FD_QUAD_ILP 0
-#endif
-#ifndef FD_QUAD_V2
-#define FD_QUAD_V2 1   /* the step layout of fd_q2_kind_bits (round 5); 0 = round 4's */
 #endif
 #ifndef FD_QUAD_DPP_AND
 #define FD_QUAD_DPP_AND 1
@@ -976,11 +1002,11 @@ FD_QDEV int fd_lat_code( int32_t const * __restrict__ status, int32_t const * __
    into LDS: every lane's loads first, then its stores.  SIGS rows of
    FD_OPS_MAX bytes in 16-byte chunks; bi: 8 entries in the kernel's layout
    (bi_at maps a Bi dword index to its LDS dword index) */
-template<int SIGS, int BI_DW, typename AT>
+template<int SIGS, int BI_DW, int ROW, int BASE, typename AT>
 FD_QDEV void fd_lat_stage( uint8_t const * __restrict__ ops, uint64_t sig0, uint64_t n, int t0,
-                           uint8_t (*lops)[FD_QOPS_ROW], int32_t * lbi, AT bi_at ) {
+                           uint8_t (*lops)[ROW], int32_t * lbi, AT bi_at ) {
   uint32_t const lane = threadIdx.x & 63u;
-  int const c0 = t0 >> 4;
+  int const c0 = (t0 > BASE ? t0 : BASE) >> 4;   /* rows hold t >= BASE (a multiple of 16) */
   constexpr int NC = (SIGS*(FD_OPS_MAX/16) + 63) / 64, NB = (BI_DW + 63) / 64;
   int4 v[NC];
 #pragma unroll
@@ -1000,7 +1026,7 @@ FD_QDEV void fd_lat_stage( uint8_t const * __restrict__ ops, uint64_t sig0, uint
 #pragma unroll
   for( int j=0; j<NC; j++ ) {
     int c = (int)lane + 64*j, sg = c / (FD_OPS_MAX/16), ch = c % (FD_OPS_MAX/16);
-    if( c < SIGS*(FD_OPS_MAX/16) && ch >= c0 ) *(int4 *)&lops[sg][ch*16] = v[j];
+    if( c < SIGS*(FD_OPS_MAX/16) && ch >= c0 ) *(int4 *)&lops[sg][ch*16 - BASE] = v[j];
   }
 #pragma unroll
   for( int j=0; j<NB; j++ ) { int k = (int)lane + 64*j; if( k < BI_DW ) lbi[bi_at.dst( k )] = b[j]; }
@@ -1037,7 +1063,14 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      ~100-deep chain of dependent round trips in front of the first step) */
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
-  fd_lat_stage<FD_QSIGS, 8*FD_TAB_ENTRY>( ops, sig0, n, t0, L.ops, L.tab[FD_QSIGS], fd_bi_quad{} );
+  fd_lat_stage<FD_QSIGS, 8*FD_TAB_ENTRY, FD_QOPS_ROWQ, FD_QOPS_BASE>( ops, sig0, n, t0, L.ops, L.tab[FD_QSIGS], fd_bi_quad{} );
+#if FD_QUAD_STEP >= 3
+  /* the step decode table: 12 entries x FD_Q3_DW dwords, 6 per lane */
+  for( uint32_t k = threadIdx.x & 63u; k < 3u*4u*FD_Q3_DW; k += 64u ) {
+    uint32_t const e = k / FD_Q3_DW, dw = k % FD_Q3_DW;
+    L.dec[k] = (int32_t)fd_q3_entry( e & 3u, (int)(e >> 2), (int)dw );
+  }
+#endif
 
   /* per-lane constant masks */
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
@@ -1079,10 +1112,12 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
      (P, Q, R, S), followed by the op's output mix */
   fd_fe_set( vt, q ? 1 : 0 );
   uint32_t const tab_bi = (uint32_t)(L.tab[FD_QSIGS] - tab_s);   /* int32s from this signature's Ai to Bi */
-#if FD_QUAD_V2
+#if FD_QUAD_STEP == 2
   /* this lane's decode words for D, positive-digit add, negative-digit add
      (fd_q2_kind_bits: the step's lane layout, masks and bias constants) */
   uint32_t const kw0 = fd_q2_kind_bits( q, 0, 0 ), kw1 = fd_q2_kind_bits( q, 1, 0 ), kw2 = fd_q2_kind_bits( q, 1, 1 );
+#elif FD_QUAD_STEP >= 3
+  int32_t const * const dec_q = L.dec + q*FD_Q3_DW;   /* + kind * 4 * FD_Q3_DW */
 #else
   uint64_t const okw = fd_op_kind_word( q );
 #endif
@@ -1093,11 +1128,22 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
        op_start (its prep lane zeroed the whole row before recoding), and
        any other row's bytes only steer lanes whose result is discarded
        (code != FD_ST_PENDING), with table indices bounded by the masks */
-    int op = (int)L.ops[ls][t];
-#if FD_QUAD_V2
+    int op = (int)L.ops[ls][t - FD_QOPS_BASE];
+#if FD_QUAD_STEP == 2
     uint32_t const madd = fd_ok_mask( (uint32_t)op, 7 ), mneg = fd_ok_mask( (uint32_t)op, 5 );
     uint32_t const kd = fd_sel( madd, fd_sel( mneg, kw2, kw1 ), kw0 );
     uint32_t idx = fd_ok_bits( kd, FD_Q2_IDX, 2 );
+#elif FD_QUAD_STEP >= 3
+    /* this lane's decode entry for the op's kind (D 0, +add 1, -add 2) */
+    uint32_t const kind = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);
+    int32_t D[FD_Q3_DW];
+    {
+      int4 const * de = (int4 const *)(dec_q + kind*(4u*FD_Q3_DW));
+#pragma unroll
+      for( int j=0; j<FD_Q3_DW/4; j++ ) { int4 x = de[j]; D[4*j] = x.x; D[4*j+1] = x.y; D[4*j+2] = x.z; D[4*j+3] = x.w; }
+    }
+    uint32_t const madd = (uint32_t)D[FD_Q3_MADD];
+    uint32_t idx = 0;   /* the entry lane's offset comes with the entry */
 #else
     uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
     uint32_t add = fd_ok_mask( kd, FD_OK_QS );
@@ -1108,12 +1154,53 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     {
       /* Bi (op bit 6) or this signature's Ai: the row offset by arithmetic,
          not a compare and select (a VALU-written SGPR mask costs wait states) */
+#if FD_QUAD_STEP >= 3
+      int32_t const * ent = tab_s + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_TAB_ENTRY + (uint32_t)D[FD_Q3_IDX];
+      (void)idx;
+#else
       int32_t const * ent = tab_s + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
+#endif
       int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
     }
 
-#if FD_QUAD_V2
+#if FD_QUAD_STEP >= 3
+    /* the step of FD_QUAD_STEP 2 (below) on raw product limbs: each limb's
+       residual mask is folded into the mask that selects it (the entry's
+       E / O variants; limbs 1 and 5 arrive materialized, class X) and its
+       bias into kf / K of its class */
+    fe Cr;
+    fd_fe_qperm<FD_QP(1,2,3,0)>( g, vt );
+    fd_fe_mul_raw( Cr, vt, g );
+    uint32_t const sA = (uint32_t)D[FD_Q3_SA], gs = (uint32_t)D[FD_Q3_GS];
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      int const cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;         /* mask: 0 E (26 bits), 1 O (25) */
+      int const kc  = !(k & 1) ? FD_Q3_KFE : (k == 1 || k == 5) ? FD_Q3_KFX : FD_Q3_KFO;
+      uint32_t const mA = (uint32_t)D[FD_Q3_MAE + cls];
+      uint32_t const mB = (uint32_t)fd_opaque( D[FD_Q3_MBE + cls] );
+      uint32_t const p  = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,2,1)>( Cr.v[k] ) & mB) );
+      uint32_t const fk = fd_andxor( (uint32_t)Cr.v[k], mA, sA ) + p + (uint32_t)D[kc];
+      f.v[k] = (int32_t)fk;
+      g.v[k] = (int32_t)fd_sel( madd, (uint32_t)E[k], fk << gs );
+    }
+    fe hr; fd_fe_mul_raw( hr, f, g );
+    uint32_t const qs = (uint32_t)D[FD_Q3_QS], sR = (uint32_t)D[FD_Q3_SR], sS = (uint32_t)D[FD_Q3_SS];
+#pragma unroll
+    for( int k=0; k<10; k++ ) {
+      int const cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;
+      int const kc  = !(k & 1) ? FD_Q3_KE : (k == 1 || k == 5) ? FD_Q3_KX : FD_Q3_KO;
+      uint32_t const mP = (uint32_t)fd_opaque( D[FD_Q3_MPE + cls] ), mQ = (uint32_t)fd_opaque( D[FD_Q3_MQE + cls] );
+      uint32_t const mR = (uint32_t)fd_opaque( D[FD_Q3_MRE + cls] ), mS = (uint32_t)fd_opaque( D[FD_Q3_MSE + cls] );
+      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( hr.v[k] ) & mP) );
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( hr.v[k] ) & mQ) );
+      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( hr.v[k] ) & mR) );
+      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( hr.v[k] ) & mS) );
+      /* (c ^ sR) + K, (d ^ sS) + a as v_xad_u32; + (b << qs) as v_lshl_add */
+      uint32_t const x1 = fd_xad( c, sR, (uint32_t)D[kc] ), x2 = fd_xad( d, sS, a );
+      vt.v[k] = (int32_t)((b << qs) + x1 + x2);
+    }
+#elif FD_QUAD_STEP == 2
     /* C = V (.) rot(V): lane q forms t_q t_{q+1}, so C = [T, Y, Z, X] and
        only g needs a quad move (X = t3 t0 takes its operands in the other
        order than the reference's t0 t3: the same exact column sums, as no
@@ -1366,7 +1453,10 @@ FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
 #endif
 FD_QDEV int32_t fd_o_partner( int32_t x ) { return __builtin_amdgcn_ds_swizzle( x, 0x401F ); }
 
-/* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9) */
+/* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9);
+   BIASED = 1 leaves each limb's carry bias in (the oct step folds it into
+   the constants of the adds that consume it, as the quad does) */
+template<int BIASED=0>
 FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c ) {
   fd_oops o;
 #if FD_OCT_SWIZZLE == 2
@@ -1444,11 +1534,12 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
     S[0] = fd_sel64( c.hm, S[0], (int64_t)(uint64_t)((uint32_t)S[0] & c.mE) );
     S[1] += cy;
   }
-  out.v[0] = fd_opaque( (int32_t)((uint32_t)S[0] - c.bE) );
-  out.v[1] = fd_opaque( (int32_t)((uint32_t)S[1] - c.bO) );
-  out.v[2] = fd_opaque( (int32_t)((uint32_t)S[2] - c.bE) );
-  out.v[3] = fd_opaque( (int32_t)((uint32_t)S[3] - c.bO) );
-  out.v[4] = fd_opaque( (int32_t)((uint32_t)S[4] - c.bE) );
+  uint32_t const bE = BIASED ? 0u : c.bE, bO = BIASED ? 0u : c.bO;
+  out.v[0] = fd_opaque( (int32_t)((uint32_t)S[0] - bE) );
+  out.v[1] = fd_opaque( (int32_t)((uint32_t)S[1] - bO) );
+  out.v[2] = fd_opaque( (int32_t)((uint32_t)S[2] - bE) );
+  out.v[3] = fd_opaque( (int32_t)((uint32_t)S[3] - bO) );
+  out.v[4] = fd_opaque( (int32_t)((uint32_t)S[4] - bE) );
 }
 
 template<int CTRL> FD_QDEV void fd_fh_qperm( fh & o, fh const & x ) {
@@ -1496,9 +1587,20 @@ struct fd_bi_oct {
   __device__ __forceinline__ int src( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_TAB_ENTRY + l*FD_TAB_LANE + limb; }
   __device__ __forceinline__ int dst( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_OTAB_ENTRY + l*FD_OTAB_LANE + (limb < 5 ? limb : limb + 3); }
 };
+/* The oct step (FD_OCT_STEP): 1 round 4's (the quad's round-4 layout on
+   half elements); 3 (default) the quad's FD_QUAD_STEP 2 layout on half
+   elements (C = V (.) rot V, own/partner operand forms, biased products)
+   with its decode read from an LDS table (fd_o3_entry) and xor-adds in
+   the mix */
+#ifndef FD_OCT_STEP
+#define FD_OCT_STEP 3
+#endif
 struct fd_oct_lds {
   int32_t tab[FD_OSIGS+1][8*FD_OTAB_ENTRY];   /* Ai per signature, [FD_OSIGS] = Bi */
   uint8_t ops[FD_OSIGS][FD_QOPS_ROW];
+#if FD_OCT_STEP >= 3
+  int32_t dec[3*4*2*FD_O3_DW];              /* fd_o3_entry per (op kind, lane q, half h) */
+#endif
 };
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -1527,7 +1629,13 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
 
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
-  fd_lat_stage<FD_OSIGS, 8*4*10>( ops, sig0, n, t0, L.ops, L.tab[FD_OSIGS], fd_bi_oct{} );
+  fd_lat_stage<FD_OSIGS, 8*4*10, FD_QOPS_ROW, 0>( ops, sig0, n, t0, L.ops, L.tab[FD_OSIGS], fd_bi_oct{} );
+#if FD_OCT_STEP >= 3
+  for( uint32_t k = threadIdx.x & 63u; k < 3u*4u*2u*FD_O3_DW; k += 64u ) {
+    uint32_t const e = k / FD_O3_DW, dw = k % FD_O3_DW;   /* e = (kind*4 + q)*2 + h */
+    L.dec[k] = (int32_t)fd_o3_entry( (e >> 1) & 3u, e & 1u, (int)(e >> 3), (int)dw, FD_OTAB_LANE );
+  }
+#endif
 
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
   uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
@@ -1563,6 +1671,63 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   }
   __syncthreads();
 
+#if FD_OCT_STEP >= 3
+  /* main loop: the quad's step (FD_QUAD_STEP 2 layout) on half field
+     elements, its decode from the LDS table */
+  int32_t const * const dec_qh = L.dec + (q*2u + h)*FD_O3_DW;   /* + kind * 8 * FD_O3_DW */
+  uint32_t const tab_bi = (uint32_t)(L.tab[FD_OSIGS] - L.tab[ls]);   /* int32s from this signature's Ai to Bi */
+  fh s;
+#pragma unroll
+  for( int k=0; k<5; k++ ) s.v[k] = 0;
+  s.v[0] = (int32_t)((q && !h) ? 1 : 0);
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long os_c0 = __builtin_amdgcn_s_memtime(), os_r0 = __builtin_amdgcn_s_memrealtime();
+  for( int t=t0; t<FD_OPS_MAX; t++ ) {
+    int op = (int)L.ops[ls][t];
+    uint32_t const kind = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);
+    int32_t D[FD_O3_DW];
+    {
+      int4 const * de = (int4 const *)(dec_qh + kind*(8u*FD_O3_DW));
+#pragma unroll
+      for( int j=0; j<FD_O3_DW/4; j++ ) { int4 x = de[j]; D[4*j] = x.x; D[4*j+1] = x.y; D[4*j+2] = x.z; D[4*j+3] = x.w; }
+    }
+    int32_t E[5];
+    {
+      int32_t const * ent = L.tab[ls] + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_OTAB_ENTRY + (uint32_t)D[FD_O3_IDX] + 8u*h;
+      int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1];
+      E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x;
+    }
+    /* C = V (.) rot V = [T, Y, Z, X], biased */
+    fh go, C;
+    fd_fh_qperm<FD_QP(1,2,3,0)>( go, s );
+    fd_o_mul<1>( C, s, go, oc );
+    /* f = a C + b C' (C' of lane 3,3,2,1), g = E (add) or f (D; q2: 2f) */
+    fh fo;
+    uint32_t const mA = (uint32_t)D[FD_O3_MA], sA = (uint32_t)D[FD_O3_SA], gs = (uint32_t)D[FD_O3_GS], madd = (uint32_t)D[FD_O3_MADD];
+    uint32_t const mB = (uint32_t)fd_opaque( D[FD_O3_MB] );
+#pragma unroll
+    for( int k=0; k<5; k++ ) {
+      uint32_t const p  = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,2,1)>( C.v[k] ) & mB) );
+      uint32_t const fk = fd_andxor( (uint32_t)C.v[k], mA, sA ) + p + (uint32_t)D[(k & 1) ? FD_O3_KFO : FD_O3_KFE];
+      fo.v[k] = (int32_t)fk;
+      go.v[k] = (int32_t)fd_sel( madd, (uint32_t)E[k], fk << gs );
+    }
+    fh hq; fd_o_mul<1>( hq, fo, go, oc );
+    /* the mix over h = [S, P, Q, R], biases in K */
+    uint32_t const qs = (uint32_t)D[FD_O3_QS], sR = (uint32_t)D[FD_O3_SR], sS = (uint32_t)D[FD_O3_SS];
+    uint32_t const mP = (uint32_t)fd_opaque( D[FD_O3_MP] ), mQ = (uint32_t)fd_opaque( D[FD_O3_MQ] );
+    uint32_t const mR = (uint32_t)fd_opaque( D[FD_O3_MR] ), mS = (uint32_t)fd_opaque( D[FD_O3_MS] );
+#pragma unroll
+    for( int k=0; k<5; k++ ) {
+      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( hq.v[k] ) & mP) );
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( hq.v[k] ) & mQ) );
+      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( hq.v[k] ) & mR) );
+      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( hq.v[k] ) & mS) );
+      uint32_t const x1 = fd_xad( c, sR, (uint32_t)D[(k & 1) ? FD_O3_KO : FD_O3_KE] ), x2 = fd_xad( d, sS, a );
+      s.v[k] = (int32_t)((b << qs) + x1 + x2);
+    }
+  }
+#else
   /* main loop: the quad's step on half field elements */
   uint64_t const okw = fd_op_kind_word( q );
   uint32_t const tab_bi = (uint32_t)(L.tab[FD_OSIGS] - L.tab[ls]);   /* int32s from this signature's Ai to Bi */
@@ -1617,6 +1782,7 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
       s.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + cadd);
     }
   }
+#endif
   fd_clk_add( 6, os_c0, os_r0, lane );
 
   /* the whole final state, then the quad's final p1p1 -> p2 and the limb

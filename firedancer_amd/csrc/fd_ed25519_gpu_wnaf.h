@@ -145,6 +145,128 @@ FD_DEV uint32_t fd_q2_kind_bits( uint32_t q, int add, int neg ) {
        | ((uint32_t)(-2*(fa + fb)) & 0xFFu)          << FD_Q2_NF;
 }
 
+/* The quad DSM's per-step decode as a table in LDS (FD_QUAD_V2 == 3): one
+   entry of FD_Q3_DW dwords per (op kind, lane q), every mask already
+   expanded and narrowed to the limb class it is applied to, so a step
+   reads its lane's entry (ds_read_b128 x 7) instead of extracting ~20
+   fields.  The products hand over RAW limbs (fd_fe_limbs_t<FD_FE_RAW>):
+   the residual masks of limbs 0, 2, 4, 6, 8 (26 bits: class E) and 3, 7, 9
+   (25 bits: class O) fold into the operand and output masks, limbs 1 and 5
+   (class X: 26-bit mask, bias 2^24 + FD_FE_RAW_X) too, and each class's
+   bias into kf / K.  Signs (sA, sR, sS) stay full masks; gs, qs are shift
+   counts; IDX is the table entry lane's offset in int32s. */
+#define FD_Q3_MAE   0
+#define FD_Q3_MAO   1
+#define FD_Q3_MBE   2
+#define FD_Q3_MBO   3
+#define FD_Q3_MPE   4
+#define FD_Q3_MPO   5
+#define FD_Q3_MQE   6
+#define FD_Q3_MQO   7
+#define FD_Q3_MRE   8
+#define FD_Q3_MRO   9
+#define FD_Q3_MSE   10
+#define FD_Q3_MSO   11
+#define FD_Q3_SA    12
+#define FD_Q3_SR    13
+#define FD_Q3_SS    14
+#define FD_Q3_GS    15
+#define FD_Q3_QS    16
+#define FD_Q3_MADD  17
+#define FD_Q3_KFE   18
+#define FD_Q3_KFO   19
+#define FD_Q3_KFX   20
+#define FD_Q3_KE    21
+#define FD_Q3_KO    22
+#define FD_Q3_KX    23
+#define FD_Q3_IDX   24
+#define FD_Q3_DW    28          /* 7 x 16 bytes */
+FD_DEV uint32_t fd_q3_entry( uint32_t q, int kind, int dw ) {
+  uint32_t w = fd_q2_kind_bits( q, kind != 0, kind == 2 );
+  uint32_t const mE = (1u<<26)-1u, mO = (1u<<25)-1u;
+  uint32_t const bE = 1u<<25, bO = 1u<<24, bX = (1u<<24) + FD_FE_RAW_X;
+  auto m = [&]( int bit ) -> uint32_t { return ((w >> bit) & 1u) ? ~0u : 0u; };
+  int32_t  sumc = -(int32_t)(int8_t)(uint8_t)(w >> FD_Q2_SUMC);
+  int32_t  nf   = -(int32_t)(int8_t)(uint8_t)(w >> FD_Q2_NF) / 2;
+  uint32_t cadd = (w >> FD_Q2_CADD) & 3u, sa1 = (w >> FD_Q2_SA) & 1u;
+  switch( dw ) {
+    case FD_Q3_MAE: return m( FD_Q2_MA ) & mE;   case FD_Q3_MAO: return m( FD_Q2_MA ) & mO;
+    case FD_Q3_MBE: return m( FD_Q2_MB ) & mE;   case FD_Q3_MBO: return m( FD_Q2_MB ) & mO;
+    case FD_Q3_MPE: return m( FD_Q2_MP ) & mE;   case FD_Q3_MPO: return m( FD_Q2_MP ) & mO;
+    case FD_Q3_MQE: return m( FD_Q2_MQ ) & mE;   case FD_Q3_MQO: return m( FD_Q2_MQ ) & mO;
+    case FD_Q3_MRE: return m( FD_Q2_MR ) & mE;   case FD_Q3_MRO: return m( FD_Q2_MR ) & mO;
+    case FD_Q3_MSE: return m( FD_Q2_MS ) & mE;   case FD_Q3_MSO: return m( FD_Q2_MS ) & mO;
+    case FD_Q3_SA:  return m( FD_Q2_SA );
+    case FD_Q3_SR:  return m( FD_Q2_SR );
+    case FD_Q3_SS:  return m( FD_Q2_SS );
+    case FD_Q3_GS:  return (w >> FD_Q2_GS) & 1u;
+    case FD_Q3_QS:  return kind ? 1u : 0u;
+    case FD_Q3_MADD:return kind ? ~0u : 0u;
+    case FD_Q3_KFE: return sa1 - (uint32_t)nf * bE;
+    case FD_Q3_KFO: return sa1 - (uint32_t)nf * bO;
+    case FD_Q3_KFX: return sa1 - (uint32_t)nf * bX;
+    case FD_Q3_KE:  return cadd - (uint32_t)sumc * bE;
+    case FD_Q3_KO:  return cadd - (uint32_t)sumc * bO;
+    case FD_Q3_KX:  return cadd - (uint32_t)sumc * bX;
+    case FD_Q3_IDX: return ((w >> FD_Q2_IDX) & 3u) * (uint32_t)FD_TAB_LANE;
+    default:        return 0u;
+  }
+}
+
+/* The eight-lane DSM's decode entries (fd_k_dsm_oct, FD_OCT_STEP 3): the
+   quad's step layout (fd_q2_kind_bits) on half field elements, per (op
+   kind, lane q, half h).  The oct's products come out biased
+   (fd_o_mul<1>): slot j of a lane is column 5h + j, whose bias is 2^25 for
+   an even column and 2^24 for an odd one, so kf / K come per slot parity
+   of the half.  Masks are full (0 / ~0); IDX is the entry lane times the
+   caller's lane stride. */
+#define FD_O3_MA    0
+#define FD_O3_SA    1
+#define FD_O3_MB    2
+#define FD_O3_GS    3
+#define FD_O3_MADD  4
+#define FD_O3_MP    5
+#define FD_O3_MQ    6
+#define FD_O3_MR    7
+#define FD_O3_SR    8
+#define FD_O3_MS    9
+#define FD_O3_SS    10
+#define FD_O3_QS    11
+#define FD_O3_KFE   12
+#define FD_O3_KFO   13
+#define FD_O3_KE    14
+#define FD_O3_KO    15
+#define FD_O3_IDX   16
+#define FD_O3_DW    20          /* 5 x 16 bytes */
+FD_DEV uint32_t fd_o3_entry( uint32_t q, uint32_t h, int kind, int dw, uint32_t lane_stride ) {
+  uint32_t w = fd_q2_kind_bits( q, kind != 0, kind == 2 );
+  auto m = [&]( int bit ) -> uint32_t { return ((w >> bit) & 1u) ? ~0u : 0u; };
+  int32_t  sumc = -(int32_t)(int8_t)(uint8_t)(w >> FD_Q2_SUMC);
+  int32_t  nf   = -(int32_t)(int8_t)(uint8_t)(w >> FD_Q2_NF) / 2;
+  uint32_t cadd = (w >> FD_Q2_CADD) & 3u, sa1 = (w >> FD_Q2_SA) & 1u;
+  uint32_t const bEs = h ? (1u<<24) : (1u<<25), bOs = h ? (1u<<25) : (1u<<24);   /* even / odd slots */
+  switch( dw ) {
+    case FD_O3_MA:   return m( FD_Q2_MA );
+    case FD_O3_SA:   return m( FD_Q2_SA );
+    case FD_O3_MB:   return m( FD_Q2_MB );
+    case FD_O3_GS:   return (w >> FD_Q2_GS) & 1u;
+    case FD_O3_MADD: return kind ? ~0u : 0u;
+    case FD_O3_MP:   return m( FD_Q2_MP );
+    case FD_O3_MQ:   return m( FD_Q2_MQ );
+    case FD_O3_MR:   return m( FD_Q2_MR );
+    case FD_O3_SR:   return m( FD_Q2_SR );
+    case FD_O3_MS:   return m( FD_Q2_MS );
+    case FD_O3_SS:   return m( FD_Q2_SS );
+    case FD_O3_QS:   return kind ? 1u : 0u;
+    case FD_O3_KFE:  return sa1 - (uint32_t)nf * bEs;
+    case FD_O3_KFO:  return sa1 - (uint32_t)nf * bOs;
+    case FD_O3_KE:   return cadd - (uint32_t)sumc * bEs;
+    case FD_O3_KO:   return cadd - (uint32_t)sumc * bOs;
+    case FD_O3_IDX:  return ((w >> FD_Q2_IDX) & 3u) * lane_stride;
+    default:         return 0u;
+  }
+}
+
 /* this lane's field for op: kind 0/1/2 = bit 7 + bit 5 */
 FD_DEV uint32_t fd_op_kind( uint64_t kw, int op ) {
   uint32_t k = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);

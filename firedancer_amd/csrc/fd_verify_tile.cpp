@@ -16,6 +16,7 @@
      completed batches, oldest first -> publish txns whose signatures all
        verified, SV_FILT the rest */
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -573,7 +574,19 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
       fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
       fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
     }
-    fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
+    /* unregister fails while a slot still DMAs from the region (a batch
+       whose bounded poll above timed out): retry for up to another engine
+       timeout, then report the registration as leaked rather than drop it
+       silently (it would keep its refcount and make a later
+       register of the same pointer with another size fail) */
+    int r = fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
+    long to = fd_ed25519_gpu_timeout( t->gpu );
+    for( long w = 0; r && (to < 0 || w < to); w += 1000000L ) {
+      struct timespec ts = { 0, 1000000L }; nanosleep( &ts, NULL );
+      r = fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
+    }
+    if( r ) fprintf( stderr, "fd_verify_tile_delete: input region %p still in use by the device: left registered (leaked)\n",
+                     (void const *)t->ip_region );
     for( fd_vt_batch * b : t->all ) { free( b->desc ); delete b; }
     fd_vt_tcache_delete( t->tc );
     delete t;

@@ -80,7 +80,7 @@ void h_fe_invert( int32_t * h, int32_t const * f, unsigned long n ) {
 /* The quad DSM (fd_quad_body in fd_ed25519_gpu_kernels.hip) restated with
    the four lanes of a signature's quad as an array: the DPP quad moves
    become index permutations, every per-lane mask and constant comes from
-   the same fd_q2_kind_bits / fd_fe_mul_b the kernel uses.  [a]A + [b]B
+   the same fd_q3_entry / fd_fe_mul_raw the kernel uses.  [a]A + [b]B
    as p2 limbs (X, Y, Z: 30 int32), for tests/test_quad_model.py to hold
    against the reference's fd_ed25519_ge_double_scalarmult_vartime limb for
    limb.  maxlimb (optional) returns the largest |limb| of any product
@@ -148,51 +148,49 @@ int h_quad_dsm( int32_t * out, int32_t const * A, uint8_t const * ops, int start
   fe bi[8][4];
   for( int e=0; e<8; e++ ) for( int q=0; q<4; q++ ) bi[e][q] = FD_GPU_BI_PRECOMP[e].l[q];
 
-  /* main loop (FD_QUAD_V2) */
-  uint32_t kw[3][4];
-  for( int q=0; q<4; q++ ) { kw[0][q] = fd_q2_kind_bits( q, 0, 0 ); kw[1][q] = fd_q2_kind_bits( q, 1, 0 ); kw[2][q] = fd_q2_kind_bits( q, 1, 1 ); }
+  /* main loop (FD_QUAD_STEP 3: the decode entries of fd_q3_entry, raw
+     product limbs with their residual masks folded into the entry's
+     masks; the same arithmetic the kernel issues, lane by lane) */
   for( int q=0; q<4; q++ ) fd_fe_set( vt[q], q ? 1 : 0 );
   int32_t mx = 0;
   for( int t=start; t<FD_OPS_MAX; t++ ) {
     int op = ops[t];
     int kind = (op >> 7) ? 1 + ((op >> 5) & 1) : 0;
-    fe Cb[4], h[4], E[4];
-    uint32_t kd[4];
+    fe Cr[4], hr[4], E[4];
+    uint32_t D[4][FD_Q3_DW];
     for( int q=0; q<4; q++ ) {
-      kd[q] = kw[kind][q];
-      uint32_t idx = fd_ok_bits( kd[q], FD_Q2_IDX, 2 );
+      for( int dw=0; dw<FD_Q3_DW; dw++ ) D[q][dw] = fd_q3_entry( (uint32_t)q, kind, dw );
+      uint32_t idx = D[q][FD_Q3_IDX] / FD_TAB_LANE;
       E[q] = ((op >> 6) & 1) ? bi[op & 7][idx] : tab[op & 7][idx];
     }
     m_perm( g, vt, 1, 2, 3, 0 );
     for( int q=0; q<4; q++ ) {
       for( int k=0; k<10; k++ ) { mx = m_abs( vt[q].v[k] ) > mx ? m_abs( vt[q].v[k] ) : mx; }
-      fd_fe_mul_b( Cb[q], vt[q], g[q] );
+      fd_fe_mul_raw( Cr[q], vt[q], g[q] );
     }
-    fe Cp[4]; m_perm( Cp, Cb, 3, 3, 2, 1 );
+    fe Cp[4]; m_perm( Cp, Cr, 3, 3, 2, 1 );
     for( int q=0; q<4; q++ ) {
-      uint32_t w = kd[q];
-      uint32_t mA = fd_ok_mask( w, FD_Q2_MA ), sA = fd_ok_mask( w, FD_Q2_SA ), mB = fd_ok_mask( w, FD_Q2_MB );
-      uint32_t kfe = w & 0xFF000001u, kfo = (uint32_t)((int32_t)(w & 0xFF000000u) >> 1) + (w & 1u);
-      uint32_t gs = fd_ok_bits( w, FD_Q2_GS, 1 ), madd = kind ? ~0u : 0u;
+      uint32_t const * d = D[q];
       for( int k=0; k<10; k++ ) {
-        uint32_t fk = (((uint32_t)Cb[q].v[k] & mA) ^ sA) + ((uint32_t)Cp[q].v[k] & mB) + ((k & 1) ? kfo : kfe);
+        int cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;
+        int kc  = !(k & 1) ? FD_Q3_KFE : (k == 1 || k == 5) ? FD_Q3_KFX : FD_Q3_KFO;
+        uint32_t fk = (((uint32_t)Cr[q].v[k] & d[FD_Q3_MAE + cls]) ^ d[FD_Q3_SA]) + ((uint32_t)Cp[q].v[k] & d[FD_Q3_MBE + cls]) + d[kc];
         f[q].v[k] = (int32_t)fk;
-        g[q].v[k] = (int32_t)fd_sel( madd, (uint32_t)E[q].v[k], fk << gs );
+        g[q].v[k] = (int32_t)fd_sel( d[FD_Q3_MADD], (uint32_t)E[q].v[k], fk << d[FD_Q3_GS] );
         mx = m_abs( f[q].v[k] ) > mx ? m_abs( f[q].v[k] ) : mx;
         mx = m_abs( g[q].v[k] ) > mx ? m_abs( g[q].v[k] ) : mx;
       }
-      fd_fe_mul_b( h[q], f[q], g[q] );
+      fd_fe_mul_raw( hr[q], f[q], g[q] );
     }
     for( int q=0; q<4; q++ ) {
-      uint32_t w = kd[q];
-      uint32_t mP = fd_ok_mask( w, FD_Q2_MP ), mQ = fd_ok_mask( w, FD_Q2_MQ ), qs = kind ? 1u : 0u;
-      uint32_t mR = fd_ok_mask( w, FD_Q2_MR ), sR = fd_ok_mask( w, FD_Q2_SR );
-      uint32_t mS = fd_ok_mask( w, FD_Q2_MS ), sS = fd_ok_mask( w, FD_Q2_SS );
-      uint32_t cadd = fd_ok_bits( w, FD_Q2_CADD, 2 ), sc = fd_ok_bits( w, FD_Q2_SUMC, 8 );
-      uint32_t Ke = (sc << 25) + cadd, Ko = (sc << 24) + cadd;
-      for( int k=0; k<10; k++ )
-        vt[q].v[k] = (int32_t)(((uint32_t)h[1].v[k] & mP) + (((uint32_t)h[2].v[k] & mQ) << qs)
-                               + (((uint32_t)h[3].v[k] & mR) ^ sR) + (((uint32_t)h[0].v[k] & mS) ^ sS) + ((k & 1) ? Ko : Ke));
+      uint32_t const * d = D[q];
+      for( int k=0; k<10; k++ ) {
+        int cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;
+        int kc  = !(k & 1) ? FD_Q3_KE : (k == 1 || k == 5) ? FD_Q3_KX : FD_Q3_KO;
+        uint32_t a = (uint32_t)hr[1].v[k] & d[FD_Q3_MPE + cls], b = (uint32_t)hr[2].v[k] & d[FD_Q3_MQE + cls];
+        uint32_t c = (uint32_t)hr[3].v[k] & d[FD_Q3_MRE + cls], e = (uint32_t)hr[0].v[k] & d[FD_Q3_MSE + cls];
+        vt[q].v[k] = (int32_t)((b << d[FD_Q3_QS]) + ((c ^ d[FD_Q3_SR]) + d[kc]) + ((e ^ d[FD_Q3_SS]) + a));
+      }
     }
   }
   /* p1p1 -> p2: X = t0 t3, Y = t1 t2, Z = t2 t3 */

@@ -156,3 +156,42 @@ def test_tiny_engine(ref, cap):
     e = fa.Engine(0, cap, 1 << 16, depth=2)
     assert (e.verify_packed(b.blob, b.desc) == exp).all()
     e.close()
+
+
+def test_direct_code_write_vs_d2h_copy(ref, tmp_path):
+    """ring batches of up to out_direct_max signatures have their
+    codes written by the DSM straight into the slot's mapped pinned memory
+    (no D2H blit), visible once the slot's done event completes.  The
+    default covers the latency path (4,096); here a child process raises it
+    to 65,536 and checks batches of 4,096 (quad DSM) and 40,000 (the
+    uniform DSM, beyond the quad's 32,768) through the ring against the
+    reference -- and against the same batches with the direct write off
+    (FD_ED25519_GPU_OUT_DIRECT_MAX=0, the D2H copy)."""
+    import os
+    import subprocess
+    import sys
+    b = corpus.adversarial(40000, 110, seed=47, invalid_frac=0.2)
+    exp = oracle_batch(ref, b)
+    np.save(tmp_path / "exp.npy", exp)
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {fa.__file__.rsplit('/', 2)[0]!r})
+import firedancer_amd as fa
+from firedancer_amd import corpus
+b = corpus.adversarial(40000, 110, seed=47, invalid_frac=0.2)
+exp = np.load({str(tmp_path / 'exp.npy')!r})
+e = fa.Engine(0, 40000, 1 << 24, depth=3)
+for n in (4096, 40000):
+    sub = corpus.Batch(b.blob, b.desc[:n])
+    for rep in range(3):
+        t = e.submit(sub.blob, sub.desc)
+        got = np.full(n, 99, np.int32)
+        assert e.poll(t, got, True)
+        assert (got == exp[:n]).all(), (n, rep, int((got != exp[:n]).sum()))
+e.close()
+print("ok")
+"""
+    for od in ("65536", "0"):
+        env = dict(os.environ, FD_ED25519_GPU_OUT_DIRECT_MAX=od)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (od, r.stdout[-1000:], r.stderr[-3000:])

@@ -1,7 +1,7 @@
-"""The quad DSM's step layout (fd_quad_body with FD_QUAD_V2,
+"""The quad DSM's step (fd_quad_body, FD_QUAD_STEP 3,
 firedancer_amd/csrc/fd_ed25519_gpu_kernels.hip) restated on the host with
 the quad's four lanes as an array (tests/fe_host_harness.cpp h_quad_dsm:
-the same fd_q2_kind_bits decode words, biased products fd_fe_mul_b and op
+the same fd_q3_entry decode table, raw products fd_fe_mul_raw and op
 stream fd_recode as the kernel) and held limb for limb against the
 reference's double-scalar multiplication, fd_ed25519_ge_double_scalarmult_
 vartime (/root/reference/src/ballet/ed25519/avx/fd_ed25519_ge.c:405-527,
@@ -133,3 +133,28 @@ def test_biased_product(harness):
     harness.h_fe_mul(P(H1), P(F), P(G), ctypes.c_ulong(len(F)))
     harness.h_fe_mul_b(P(H2), P(F), P(G), ctypes.c_ulong(len(F)))
     assert (H1 == H2).all()
+
+
+def test_op_streams_start_inside_the_lds_rows(harness):
+    """The quad DSM keeps op rows from t = 144 on (FD_QOPS_BASE): a stream
+    of two scalars below 2^253 holds at most 2 x 51 width-5 digits, so it
+    starts at 512 - 256 - 102 = 154 or later.  Checked on random scalars and
+    on the densest patterns (every bit set, alternating bits, a digit every
+    fifth bit) at the top of the range."""
+    rng = np.random.default_rng(31)
+    dense = [2**253 - 1, int("01" * 126, 2), int("10" * 126, 2), sum(1 << (5 * i) for i in range(51)),
+             sum(1 << (5 * i + 4) for i in range(50)), L_ORDER - 1, int("1" * 252 + "0", 2)]
+    cases = [(a, b) for a in dense for b in dense]
+    cases += [(int(rng.integers(0, 2**63)) << 189 | int(rng.integers(0, 2**63)), int(rng.integers(0, 2**62)) << 190) for _ in range(500)]
+    low = FD_OPS_MAX
+    for a, b in cases:
+        a %= 2**253
+        b %= 2**253
+        ops = np.zeros(FD_OPS_MAX, np.uint8)
+        start = np.zeros(1, np.int32)
+        A = np.frombuffer(a.to_bytes(32, "little"), np.uint8).copy()
+        B = np.frombuffer(b.to_bytes(32, "little"), np.uint8).copy()
+        harness.h_recode(P(ops), P(start), P(B), P(A), ctypes.c_ulong(1))
+        low = min(low, int(start[0]))
+        assert int(start[0]) >= 154, (hex(a), hex(b), int(start[0]))
+    assert low < 200

@@ -11,6 +11,14 @@ callback (native) histograms tsorig -> tspub; --curve 4096,16384,...
 prints one such point per batch size.  --multi: ONE tile in the
 multi-engine feeder mode over all the engines (fd_verify_tile_new_multi).
 
+--check-window W: before the timed stream, the first W frags of the set go
+through a collecting tile of the same layout (engines, mode, batch size)
+and the line records what it published (the ordered ctl = frag indices,
+as a sha256 and a count) and its counters; tests/test_c5_record.py holds
+that record against the reference's per-frag semantics
+(fd_frank_verify_synth_load.c:360-410: its tcache and fd_ed25519_verify)
+on the same frags, regenerated from the seed.
+
 Multi-GPU, one process: --gpus N runs --tiles tiles on each of devices
 0..N-1 (tile k on device k mod N), every tile an independent replica on
 its own engine, ring and frag stream (no collective on the data path).
@@ -44,6 +52,8 @@ def main():
     ap.add_argument("--latency", action="store_true",
                     help="stamp tsorig at each frag's receipt and report tsorig -> tspub percentiles (native histogram)")
     ap.add_argument("--curve", default="", help="comma-separated batch sizes: one latency point per size (implies --latency)")
+    ap.add_argument("--check-window", type=int, default=0,
+                    help="record the publish stream of the first W frags (tests/test_c5_record.py checks it)")
     a = ap.parse_args()
     if a.curve:
         a.latency = True
@@ -88,6 +98,20 @@ def run(a):
     devs = [local if world > 1 else (k % a.gpus) % max(ndev, 1) for k in range(a.tiles * a.gpus)]
     engs = [fa.Engine(d, max_sigs=a.batch, max_blob=a.batch * 1400, depth=a.depth) for d in devs]
     from firedancer_amd.tile import LatHist
+    check = None
+    if a.check_window:
+        # the sample window: a collecting tile of the same layout over the
+        # first W frags (fresh tcache), published ctl (= frag index) in order
+        W = min(a.check_window, len(frags))
+        ct = VerifyTile(engs if a.multi else engs[0], batch_sigs=a.batch, collect=True,
+                        region=base if a.inplace else None)
+        ct.rx_burst(base, off[:W], sz[:W], ctl=np.arange(W, dtype=np.uint64))
+        ct.service(flush=True)
+        pub_ctl = np.array([p[2] for p in ct.published], np.uint64)
+        import hashlib
+        check = {"frags": W, "published": int(len(pub_ctl)), "pub_ctl_sha256": hashlib.sha256(pub_ctl.tobytes()).hexdigest(),
+                 "diag": {k: int(v) for k, v in ct.diag().items()}, "seed": 77 + rank, "sigs": a.sigs}
+        ct.close()
     if a.multi:       # one tile, every engine behind its feeder
         lats = [LatHist()] if a.latency else [None]
         tiles = [VerifyTile(engs, batch_sigs=a.batch, collect=False, lat=lats[0], region=base if a.inplace else None)]
@@ -157,6 +181,7 @@ def run(a):
                           "sv_filt_per_pass": int(d0["SV_FILT_CNT"]),
                           "multi_engine_tile": bool(a.multi), "inplace": bool(a.inplace), "engines": len(engs),
                           "latency_tsorig_to_tspub": lat_summary(lats) if a.latency else None,
+                          "check_window": check,
                           "diag": d1}), flush=True)
     for tile in tiles:
         tile.close()
