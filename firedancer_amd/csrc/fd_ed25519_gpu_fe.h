@@ -261,7 +261,7 @@ FD_DEV void fd_cols_ab( CA const & ca, CB const & cb, int64_t & a1, int64_t & b1
    two columns of each product run together where the carry order allows
    (four chains, every MAC three instructions after the one it depends
    on); 7 and 9 run as two chains. */
-template<typename CA, typename CB>
+template<typename CA, typename CB, int BA=0, int BB=0>
 FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, CA const & ca, CB const & cb ) {
   int64_t a0 = FD_KEVEN, b0 = FD_KEVEN, a4 = FD_KEVEN, b4 = FD_KEVEN;
   fd_cols_ab<CA,CB,0,4>( ca, cb, a0, b0, a4, b4 );
@@ -278,8 +278,8 @@ FD_DEV void fd_fe_chain2( fd_gpu_fe_t & oa, fd_gpu_fe_t & ob, CA const & ca, CB 
   a8 += a7 >> 25; b8 += b7 >> 25;
   int64_t a9 = a8 >> 26, b9 = b8 >> 26;
   fd_cols_ab<CA,CB,9,-1>( ca, cb, a9, b9, u0, u1 );
-  fd_fe_limbs( oa, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
-  fd_fe_limbs( ob, b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+  fd_fe_limbs_t<BA>( oa, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
+  fd_fe_limbs_t<BB>( ob, b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
 }
 
 /* Three independent products, column by column with the three chains
@@ -450,18 +450,21 @@ FD_DEV void fd_fe_mul_ilp( fd_gpu_fe_t & h, fd_gpu_fe_t const & f, fd_gpu_fe_t c
   fd_fe_carry( h, S );
 }
 
-/* ha = fa*ga and hb = fb*gb, interleaved (fd_mul_cols2) */
+/* ha = fa*ga and hb = fb*gb, interleaved (fd_mul_cols2); BA / BB = 1:
+   that product's limbs with their biases left in */
+template<int BA=0, int BB=0>
 FD_DEV void fd_fe_mul2_pre( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int32_t const (&fa2)[10], fd_gpu_fe_t const & ga, int32_t const (&ga19)[10],
                             fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int32_t const (&fb2)[10], fd_gpu_fe_t const & gb, int32_t const (&gb19)[10] ) {
   fd_mul_cols ca = { fa.v, fa2, ga.v, ga19 }, cb = { fb.v, fb2, gb.v, gb19 };
-  fd_fe_chain2( ha, hb, ca, cb );
+  fd_fe_chain2<fd_mul_cols, fd_mul_cols, BA, BB>( ha, hb, ca, cb );
 }
+template<int BA=0, int BB=0>
 FD_DEV void fd_fe_mul2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, fd_gpu_fe_t const & ga,
                         fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, fd_gpu_fe_t const & gb ) {
   int32_t fa2[10], ga19[10], fb2[10], gb19[10];
   fd_fe_pre_f( fa2, fa ); fd_fe_pre_g( ga19, ga );
   fd_fe_pre_f( fb2, fb ); fd_fe_pre_g( gb19, gb );
-  fd_fe_mul2_pre( ha, fa, fa2, ga, ga19, hb, fb, fb2, gb, gb19 );
+  fd_fe_mul2_pre<BA, BB>( ha, fa, fa2, ga, ga19, hb, fb, fb2, gb, gb19 );
 }
 
 /* h = n*f^2, n in {1,2}, with the AVX SQN operand convention
@@ -495,10 +498,12 @@ FD_DEV void fd_fe_sqn( fd_gpu_fe_t & h, fd_gpu_fe_t const & fe, int n ) {
   fd_fe_chain( h, o.cols( n ) );
 }
 
-/* two independent squarings ha = na*fa^2, hb = nb*fb^2, interleaved */
+/* two independent squarings ha = na*fa^2, hb = nb*fb^2, interleaved;
+   B = 1: both with their limb biases left in (fd_fe_limbs_t<1>) */
+template<int B=0>
 FD_DEV void fd_fe_sqn2( fd_gpu_fe_t & ha, fd_gpu_fe_t const & fa, int na, fd_gpu_fe_t & hb, fd_gpu_fe_t const & fb, int nb ) {
   fd_sq_ops oa, ob; oa.set( fa ); ob.set( fb );
-  fd_fe_chain2( ha, hb, oa.cols( na ), ob.cols( nb ) );
+  fd_fe_chain2<fd_sq_cols, fd_sq_cols, B, B>( ha, hb, oa.cols( na ), ob.cols( nb ) );
 }
 
 FD_DEV void fd_fe_sq( fd_gpu_fe_t & h, fd_gpu_fe_t const & f ) { fd_fe_sqn( h, f, 1 ); }

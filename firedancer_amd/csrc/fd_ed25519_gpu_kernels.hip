@@ -1329,6 +1329,14 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   if( live && q == 0u ) out[i] = code;
 }
 
+/* diagnostic builds only (FD_PREP_DYN_LDS > 0, tools/gpu.sh pmcprep):
+   extra dynamic LDS per fd_k_prep block so one block (4 waves) fills a
+   CU -- one wave per SIMD instead of four -- to split the prep's wave
+   cycles into its own dependency waits and the other waves' turns */
+#ifndef FD_PREP_DYN_LDS
+#define FD_PREP_DYN_LDS 0
+#endif
+
 extern "C" __global__ void __launch_bounds__(64)
 fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
@@ -1920,6 +1928,30 @@ fd_k_dsm_setup( uint64_t n, int32_t const * __restrict__ status, int32_t const *
 
 /* D step: p1p1 -> p2 ([X,Y,Z] = [t0 t3, t1 t2, t2 t3], avx/fd_ed25519_ge.c:
    521-522), then DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)) (:493-498) */
+/* FD_POOL_BIASED 1 (default): the products whose limbs feed only the
+   lane mixes (the doubling's four squarings; an addition's X, Y and its
+   four op products) hand them over with their carry biases in
+   (fd_fe_limbs_t<1>: one instruction fewer per limb), and the mixes, which
+   add three operands anyway, fold the biases into constants: 40 VALU
+   fewer per doubling, 60 per addition.  Limbs that feed a product stay
+   exact.  beta_k = 2^25 (even k) / 2^24 (odd k). */
+#ifndef FD_POOL_BIASED
+#define FD_POOL_BIASED 1
+#endif
+#define FD_BETA(k) ((k) & 1 ? (1u<<24) : (1u<<25))
+/* DBL_MIX [a-b-c, b+c, b-c, d-b+c] on biased a, b, c, d:
+   t = b + c + beta (one v_add3), out0 = a - t, out1 = t - beta, out2 = b - c,
+   out3 = d - b + c - beta */
+FD_DEV void v_dbl_mix_b( fe4 & h ) {
+#pragma unroll
+  for( int k=0; k<10; k++ ) {
+    uint32_t const bt = FD_BETA( k );
+    uint32_t a=h.l[0].v[k], b=h.l[1].v[k], c=h.l[2].v[k], d=h.l[3].v[k];
+    uint32_t t = b + c - bt;
+    h.l[0].v[k]=(int32_t)(a - t); h.l[1].v[k]=(int32_t)(t - bt); h.l[2].v[k]=(int32_t)(b - c); h.l[3].v[k]=(int32_t)(d - b + c - bt);
+  }
+}
+
 FD_DEV void fd_pool_dbl( fe4 & vt ) {
   fe Z, Y, X;
   {
@@ -1930,9 +1962,15 @@ FD_DEV void fd_pool_dbl( fe4 & vt ) {
     fd_fe_chain3( Z, X, Y, cz, cx, cy );
   }
   fe xy; fd_fe_add( xy, X, Y );
+#if FD_POOL_BIASED
+  fd_fe_sqn2<1>( vt.l[0], xy, 1, vt.l[1], Y, 1 );
+  fd_fe_sqn2<1>( vt.l[2], X, 1, vt.l[3], Z, 2 );
+  v_dbl_mix_b( vt );
+#else
   fd_fe_sqn2( vt.l[0], xy, 1, vt.l[1], Y, 1 );
   fd_fe_sqn2( vt.l[2], X, 1, vt.l[3], Z, 2 );
   v_dbl_mix( vt );
+#endif
 }
 
 /* A step: p1p1 -> p3 ([Z,Y,X,T], :506-508) then
@@ -1947,25 +1985,40 @@ FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, uint64_t estri
     fd_fe_pre_g( g3, vt.l[3] );
     fd_fe_pre_f( f0, vt.l[0] );
     { int32_t f2[10]; fd_fe_pre_f( f2, vt.l[2] );
-      fd_fe_mul2_pre( Z, vt.l[2], f2, vt.l[3], g3, X, vt.l[0], f0, vt.l[3], g3 ); }
+      fd_fe_mul2_pre<0, FD_POOL_BIASED>( Z, vt.l[2], f2, vt.l[3], g3, X, vt.l[0], f0, vt.l[3], g3 ); }
     { int32_t f1[10], g2[10], g1[10]; fd_fe_pre_f( f1, vt.l[1] ); fd_fe_pre_g( g2, vt.l[2] ); fd_fe_pre_g( g1, vt.l[1] );
-      fd_fe_mul2_pre( Y, vt.l[1], f1, vt.l[2], g2, T, vt.l[0], f0, vt.l[1], g1 ); }
+      fd_fe_mul2_pre<FD_POOL_BIASED, 0>( Y, vt.l[1], f1, vt.l[2], g2, T, vt.l[0], f0, vt.l[1], g1 ); }
   }
   fe h0, h1, h2, h3;   /* P, Q, R, S */
   {
     fe xy, ymx;
+#if FD_POOL_BIASED
+    /* X, Y biased: X + Y - 2 beta, Y - X (the biases cancel) */
+#pragma unroll
+    for( int k=0; k<10; k++ ) xy.v[k] = (int32_t)((uint32_t)X.v[k] + (uint32_t)Y.v[k] - 2u*FD_BETA( k ));
+#else
     fd_fe_add( xy, X, Y );
+#endif
     fd_fe_sub( ymx, Y, X );
-    fd_fe_mul2( h0, xy, E2, h1, Z, E0 );
-    fd_fe_mul2( h2, ymx, E1, h3, T, E3 );
+    fd_fe_mul2<FD_POOL_BIASED, FD_POOL_BIASED>( h0, xy, E2, h1, Z, E0 );
+    fd_fe_mul2<FD_POOL_BIASED, FD_POOL_BIASED>( h2, ymx, E1, h3, T, E3 );
   }
   uint32_t mp = (uint32_t)fd_opaque( -(int32_t)!((op >> 5) & 1) );   /* positive digit: swap out lanes 2,3 */
 #pragma unroll
   for( int k=0; k<10; k++ ) {
     uint32_t P = h0.v[k], Q = h1.v[k], R = h2.v[k], S = h3.v[k];
+#if FD_POOL_BIASED
+    /* biased P, Q, R, S: P - R, P + R - 2 beta; Q2' = 2Q - beta (one
+       v_lshl_add), o2 = Q2' - S, o3 = Q2' + S - 2 beta */
+    uint32_t const bt = FD_BETA( k );
+    uint32_t Q2 = 2u*Q - bt, o2 = Q2 - S, o3 = Q2 + S - 2u*bt;
+    vt.l[0].v[k] = (int32_t)(P - R);
+    vt.l[1].v[k] = (int32_t)(P + R - 2u*bt);
+#else
     uint32_t Q2 = 2u*Q, o2 = Q2 - S, o3 = Q2 + S;
     vt.l[0].v[k] = (int32_t)(P - R);
     vt.l[1].v[k] = (int32_t)(P + R);
+#endif
     vt.l[2].v[k] = (int32_t)fd_sel( mp, o3, o2 );
     vt.l[3].v[k] = (int32_t)fd_sel( mp, o2, o3 );
   }
@@ -2342,7 +2395,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
                         w->pstat, w->pts, portable, strict, fp, w->sdig, tag );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
-    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
+    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), FD_PREP_DYN_LDS, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
                         (uint64_t *)NULL );
     if( ev ) hipEventRecord( ev[1], stream );
     hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );

@@ -7,13 +7,17 @@
 #     test[=pytest -k expr]   the -m gpu suite (default: all of it)
 #     smoke                   __graft_entry__.smoke()
 #     bench[=bench.py args]   bench.py -> gpurun_out/bench.json
+#     libbench=lib            bench.py --no-cpu --no-latency on a variant library (appends gpurun_out/bench_<lib>.jsonl)
 #     prof                    rocprofv3 --kernel-trace --stats of a short bench
 #     abquad=lib1,lib2[,..]   tools/ab_quad.py over library variants (2 rounds)
 #     pmcquad=lib             PMC pass (VALU instr, wave cycles, clock) of a lone
 #                             4,096-signature quad batch on that library
 #     pmcthr                  PMC passes over the throughput step (VALU, FETCH, WRITE)
+#     pmcsq=lib               the SQ pass alone over the throughput step on a variant library
 #     ringpaced[=args]        tools/ring_paced.py (open-loop 4,096-batch ring)
 #     py=script[,args]        any tools/*.py under a 300 s limit
+#     libpy=lib:script[,args] the same with FD_ED25519_LIB=lib (a variant library)
+#     native=prog[,args]      tools/build/prog (tools/Makefile) under a 300 s limit
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
@@ -46,6 +50,11 @@ for step in "$@"; do
       timeout -k 10 600 python3 -u bench.py $arg > gpurun_out/bench.json 2> gpurun_out/bench.err \
         || { echo BENCH FAILED; tail -30 gpurun_out/bench.err; exit 1; }
       cut -c1-600 gpurun_out/bench.json ;;
+    libbench)
+      tag=$(basename "$arg" .so)
+      FD_ED25519_LIB=$R/$arg timeout -k 10 300 python3 -u bench.py --no-cpu --no-latency >> "gpurun_out/bench_$tag.jsonl" 2>> "gpurun_out/bench_$tag.err" \
+        || { echo "LIBBENCH $arg FAILED"; tail -20 "gpurun_out/bench_$tag.err"; exit 1; }
+      tail -1 "gpurun_out/bench_$tag.jsonl" | cut -c1-300 ;;
     prof)
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
           -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --no-latency > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" ) \
@@ -67,6 +76,10 @@ for step in "$@"; do
       pmc thr_p1 "$lib" $P1 -- "${B[@]}" || exit 1
       pmc thr_fetch "$lib" FETCH_SIZE -- "${B[@]}" || exit 1
       pmc thr_write "$lib" WRITE_SIZE -- "${B[@]}" || exit 1 ;;
+    pmcsq)
+      mkdir -p gpurun_out/pmc
+      tag=$(basename "$arg" .so)
+      pmc "sq_${tag}" "$R/$arg" $P1 -- "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-latency || exit 1 ;;
     ringpaced)
       timeout -k 10 600 python3 -u tools/ring_paced.py ${arg//,/ } >> gpurun_out/ring_paced.jsonl 2> gpurun_out/ring_paced.err \
         || { echo RINGPACED FAILED; tail -20 gpurun_out/ring_paced.err; exit 1; }
@@ -77,6 +90,17 @@ for step in "$@"; do
       timeout -k 10 300 python3 -u "tools/$script" ${rest//,/ } > "$out.out" 2> "$out.err" \
         || { echo "PY $script FAILED"; tail -20 "$out.err"; exit 1; }
       tail -20 "$out.out" ;;
+    libpy)
+      lib=${arg%%:*}; rest=${arg#*:}; script=${rest%%,*}; args=""; [[ $rest == *,* ]] && args=${rest#*,}
+      out=gpurun_out/$(basename "$script" .py).$(basename "$lib" .so)
+      FD_ED25519_LIB=$R/$lib timeout -k 10 300 python3 -u "tools/$script" ${args//,/ } >> "$out.out" 2>> "$out.err" \
+        || { echo "LIBPY $script $lib FAILED"; tail -20 "$out.err"; exit 1; }
+      tail -3 "$out.out" ;;
+    native)
+      prog=${arg%%,*}; args=""; [[ $arg == *,* ]] && args=${arg#*,}
+      timeout -k 10 300 "tools/build/$prog" ${args//,/ } >> "gpurun_out/$prog.jsonl" 2>> "gpurun_out/$prog.err" \
+        || { echo "NATIVE $prog FAILED"; tail -20 "gpurun_out/$prog.err"; exit 1; }
+      tail -4 "gpurun_out/$prog.jsonl" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done

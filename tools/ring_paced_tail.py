@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Where the paced C2 ring's sched -> done tail comes from: one offered load
+(bench.ring_stream's open loop: a 4,096-signature batch every period on the
+depth-8 ring, C3-mix corpus), every job's stamps split into
+  sched -> push    the producer's own lateness
+  push -> pick     the feeder thread taking the job
+  pick -> submit   a free ring slot (full ring: waiting for a completion)
+                   + staging and enqueue
+  submit -> done   H2D, front end, DSM, codes on the host, the feeder
+                   noticing
+with p50 / p99 of each and the mean of each over the slowest 1 % of jobs.
+usage: ring_paced_tail.py [M verifies/s (36)] [batches (4000)] [depth (8)]"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    mps = float(sys.argv[1]) if len(sys.argv) > 1 else 36.0
+    nb = int(sys.argv[2]) if len(sys.argv) > 2 else 4000
+    depth = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    import torch  # noqa: F401  (one HIP runtime)
+    import bench
+    import firedancer_amd as fa
+    from firedancer_amd import corpus
+    ring = corpus.c3_windows(bench.RING_WINDOWS, bench.BATCH_SIGS, seed=4242, nthreads=min(16, os.cpu_count() or 8))
+    eng = fa.Engine(0, max_sigs=bench.BATCH_SIGS, max_blob=8 << 20, depth=depth)
+    eng.register(ring.blob)
+    feeder = fa.Feeder(eng)
+    B = bench.BATCH_SIGS
+    starts = np.random.default_rng(7).permutation(len(ring) // B).astype(np.uint64) * B
+    period = int(round(B / (mps * 1e6) * 1e9))
+    st = feeder.synth(ring.blob, ring.desc, B, starts, nb, 2 * depth, period)
+    feeder.close()
+    eng.close()
+    st = st[2 * depth:]
+    comp = {
+        "sched_to_push": (st["t_push_ns"].astype(np.int64) - st["t_sched_ns"].astype(np.int64)) * 1e-6,
+        "push_to_pick": (st["t_pick_ns"].astype(np.int64) - st["t_push_ns"].astype(np.int64)) * 1e-6,
+        "pick_to_submit": (st["t_submit_ns"].astype(np.int64) - st["t_pick_ns"].astype(np.int64)) * 1e-6,
+        "submit_to_done": (st["t_done_ns"].astype(np.int64) - st["t_submit_ns"].astype(np.int64)) * 1e-6,
+    }
+    tot = (st["t_done_ns"].astype(np.int64) - st["t_sched_ns"].astype(np.int64)) * 1e-6
+    slow = tot >= np.percentile(tot, 99)
+    out = {"offered_mps": mps, "batches": int(len(st)), "depth": depth,
+           "sched_to_done": {"p50": float(np.percentile(tot, 50)), "p99": float(np.percentile(tot, 99)), "max": float(tot.max())}}
+    for k, v in comp.items():
+        out[k] = {"p50": float(np.percentile(v, 50)), "p99": float(np.percentile(v, 99)), "slow1pct_mean": float(v[slow].mean())}
+    # completions per 1 ms bin: a host stall shows as an empty bin while jobs are outstanding
+    done = np.sort(st["t_done_ns"].astype(np.int64))
+    gaps = np.diff(done) * 1e-6
+    out["completion_gap_ms"] = {"p50": float(np.percentile(gaps, 50)), "p99": float(np.percentile(gaps, 99)), "max": float(gaps.max())}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
