@@ -132,6 +132,25 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 #include "fd_ed25519_gpu_wnaf.h"
 #include <atomic>
 
+/* FD_PREP_ZERO 1: fd_prep_body zeroes the step-major op column it owns
+   (rows FD_OPS_ZBASE..511) instead of a memset of the whole array before
+   the launch (0, the default).  Measured on one box
+   (profiles/r05_prep_zero_ab.jsonl): the prep itself runs 1.31 -> 1.26 ms
+   (its recoder's byte stores land on lines its zero stores just wrote),
+   but the pipelined step grows 15.78 -> 15.89 ms -- the zero stores run
+   beside the previous launch's pool, the memset's 0.1 ms does not hurt it
+   -- so the memset stays. */
+#ifndef FD_PREP_ZERO
+#define FD_PREP_ZERO 0
+#endif
+#define FD_OPS_ZBASE 144
+/* threads per fd_k_prep block (64: each wave's 9 KB stage freed when that
+   wave ends rather than when the slowest of four does; no faster, same
+   A/B) */
+#ifndef FD_PREP_WG
+#define FD_PREP_WG 256
+#endif
+
 static __device__ __forceinline__ void
 fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
               fd_ed25519_gpu_desc_t const * __restrict__ desc,
@@ -186,13 +205,23 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
      quad DSM, which copies its 16 signatures' streams to LDS as 16-byte
      rows (fd_quad_body) */
   if( sigmajor ) {
-    /* the signature's own 512-byte row is zeroed here (the step-major
-       layout is zeroed by a memset before the launch; this one needs none,
-       so a small batch's front end is one launch) */
+    /* the signature's own 512-byte row is zeroed here, so a small batch's
+       front end is one launch */
     int4 * row = (int4 *)(ops + i*FD_OPS_MAX);
 #pragma unroll
     for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
   }
+#if FD_PREP_ZERO
+  else {
+    /* step-major: this signature's column from t = FD_OPS_ZBASE on (a
+       stream starts at t >= 154, tests/test_quad_model.py; the DSMs read
+       from op_start on), one byte per row -- each row's 64 bytes of a wave
+       are one coalesced store.  Replaces a memset of the whole [512][n]
+       array before the launch. */
+#pragma unroll 8
+    for( int t=FD_OPS_ZBASE; t<FD_OPS_MAX; t++ ) ops[(uint64_t)t*n + i] = 0;
+  }
+#endif
   /* the two-pass recoder, S's digits parked in this lane's slots of the
      wave's SHA-512 stage (free once the digest is out) */
   typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -347,11 +376,11 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
 #endif
 }
 
-extern "C" __global__ void __launch_bounds__(256, 4)
+extern "C" __global__ void __launch_bounds__(FD_PREP_WG, 4)
 fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
            uint64_t * __restrict__ kout ) {
-  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[4*FD_SHA_STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[(FD_PREP_WG/64)*FD_SHA_STAGE_BYTES];
   fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, kout, 0 );
 }
 
@@ -1330,8 +1359,8 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
 }
 
 /* diagnostic builds only (FD_PREP_DYN_LDS > 0, tools/gpu.sh pmcprep):
-   extra dynamic LDS per fd_k_prep block so one block (4 waves) fills a
-   CU -- one wave per SIMD instead of four -- to split the prep's wave
+   extra dynamic LDS per fd_k_prep block (built with FD_PREP_WG 256) so
+   one block (4 waves) fills a CU -- one wave per SIMD instead of four -- to split the prep's wave
    cycles into its own dependency waits and the other waves' turns */
 #ifndef FD_PREP_DYN_LDS
 #define FD_PREP_DYN_LDS 0
@@ -2374,10 +2403,10 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   if( ev ) hipEventRecord( ev[0], stream );
   /* the quad and oct DSMs share the latency front end (signature-major op rows) */
   int quad = n < pool_min && !portable && (n <= quad_max || n <= oct_max);
-  /* step-major op streams are zero-filled first; the quad schedule's
-     signature-major rows are zeroed by their own prep lanes (only rows of
-     signatures still pending after the S check are ever read) */
-  if( !quad ) {
+  /* op streams are zeroed by their own prep lanes (only rows of
+     signatures still pending after the S check are ever read); the
+     FD_PREP_ZERO 0 build memsets the step-major array first */
+  if( !quad && !FD_PREP_ZERO ) {
     hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
     if( e != hipSuccess ) return e;
   }
@@ -2395,7 +2424,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
                         w->pstat, w->pts, portable, strict, fp, w->sdig, tag );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
-    hipLaunchKernelGGL( fd_k_prep,   dim3(nb),  dim3(256), FD_PREP_DYN_LDS, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
+    hipLaunchKernelGGL( fd_k_prep,   dim3((unsigned)((n + FD_PREP_WG - 1) / FD_PREP_WG)), dim3(FD_PREP_WG), FD_PREP_DYN_LDS, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
                         (uint64_t *)NULL );
     if( ev ) hipEventRecord( ev[1], stream );
     hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
@@ -2465,9 +2494,11 @@ extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * 
                                                    fd_ed25519_gpu_desc_t const * desc, fd_ed25519_gpu_work_t const * w,
                                                    uint64_t * kout, hipStream_t stream ) {
   if( !n ) return hipSuccess;
-  hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
-  if( e != hipSuccess ) return e;
-  hipLaunchKernelGGL( fd_k_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, blob, blob_sz, desc,
+  if( !FD_PREP_ZERO ) {
+    hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+    if( e != hipSuccess ) return e;
+  }
+  hipLaunchKernelGGL( fd_k_prep, dim3((unsigned)((n + FD_PREP_WG - 1) / FD_PREP_WG)), dim3(FD_PREP_WG), 0, stream, n, blob, blob_sz, desc,
                       w->status, w->ops, w->op_start, 0, kout );
   return hipGetLastError();
 }

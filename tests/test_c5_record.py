@@ -20,6 +20,8 @@ RECORD = os.path.join(ROOT, "profiles", "r05_tile_c5_60s.jsonl")
 
 
 def _record():
+    if not os.path.exists(RECORD):
+        pytest.skip("no C5 record yet (tools/bench_tile.py --check-window on the GPU box)")
     rows = [json.loads(x) for x in open(RECORD) if x.strip().startswith("{")]
     rows = [r for r in rows if r.get("check_window")]
     assert rows, "no record with a check window"
