@@ -97,28 +97,21 @@ PEAK_INT32_OPS = 256 * 4 * 32 * PEAK_CLOCK_GHZ * 1e9   # 256 CUs x 4 SIMD x 32 l
 ALGO_BYTES_PER_SIG = 1260
 
 
-def lib_sha16(path):
-    """first 16 hex digits of the sha256 of a library file"""
-    import hashlib
-    h = hashlib.sha256()
-    with open(path, "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 20), b""):
-            h.update(chunk)
-    return h.hexdigest()[:16]
 
 
-def load_traffic(path, n_step, kernel, sha):
+def load_traffic(path, n_step, kernel, kid):
     """roofline.traffic from a PMC summary (tools/pmc_summary.py), only if it
-    was measured on THIS library build and launch size: a summary of another
-    build describes kernels that may no longer exist (round-4 verdict)."""
+    was measured on THIS device-code build (fd_ed25519_gpu_kernels_id: the
+    kernel sources and flags) and launch size: a summary of another build
+    describes kernels that may no longer exist (round-4 verdict)."""
     if not os.path.exists(path):
         return None, "no PMC summary"
     try:
         tr = json.load(open(path))
     except (OSError, ValueError):
         return None, "unreadable PMC summary"
-    if tr.get("lib_sha16") != sha:
-        return None, f"stale: PMC summary of library {tr.get('lib_sha16')}, loaded {sha}"
+    if tr.get("kernels_id") != kid:
+        return None, f"stale: PMC summary of kernels build {tr.get('kernels_id')}, loaded {kid}"
     if tr.get("sigs_per_launch") != n_step:
         return None, f"PMC summary of {tr.get('sigs_per_launch')} signatures per launch, this run {n_step}"
     v = tr.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
@@ -452,7 +445,7 @@ def main():
             kern[name] = {"ms": float(ms), "achieved_Tops": ach, "frac": ach * 1e12 / PEAK_INT32_OPS,
                           "ms_serial": float(ms1), "frac_serial": ach1 * 1e12 / PEAK_INT32_OPS}
         dom = max(kern, key=lambda k: kern[k]["ms_serial"])     # the kernel with the most work
-        traffic, traffic_status = load_traffic(a.traffic, n_step, dom, lib_sha16(fa.LIB_PATH))
+        traffic, traffic_status = load_traffic(a.traffic, n_step, dom, fa.kernels_id())
         w_total = SLOTS_DSM + SLOTS_DECOMP + SLOT_SHA_BLOCK * blocks + SLOTS_PREP_FIXED
         res["roofline"] = {
             "bound": "valu-int32",

@@ -652,6 +652,13 @@ def device_count() -> int:
     return lib().fd_ed25519_gpu_device_cnt()
 
 
+def kernels_id() -> str:
+    """build id of the loaded library's device code (fd_ed25519_gpu_kernels_id)"""
+    f = lib().fd_ed25519_gpu_kernels_id
+    f.restype = ctypes.c_char_p
+    return f().decode()
+
+
 def numa_cpus(device: int) -> list:
     """CPUs of the device's NUMA node this process may use ([] if unknown)."""
     node = lib().fd_ed25519_gpu_device_numa_node(device)

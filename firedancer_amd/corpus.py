@@ -459,3 +459,24 @@ def c3_windows(nwin, batch_sigs, seed, extra=None, extra_at=None, invalid_frac=0
         b = Batch(b.blob, b.desc[full], b.label[full])
     return b
 
+
+
+def c5_check_edits(frags):
+    """The C5 check window's adversarial edits (tools/bench_tile.py
+    --check-window, tests/test_c5_record.py), deterministic by index: frag i
+    with i % 97 == 3 gets one bit of its first signature's R flipped
+    (rejected by the verify), i % 89 == 5 repeats frag i - 1 (a dedup hit
+    when that one was not itself rejected), i % 211 == 7 declares a 3-byte
+    payload (does not parse)."""
+    import struct
+    out = list(frags)
+    for i, f in enumerate(out):
+        if i % 97 == 3:
+            b = bytearray(f)
+            b[1 + 10] ^= 0x04
+            out[i] = bytes(b)
+        elif i % 89 == 5 and i:
+            out[i] = out[i - 1]
+        elif i % 211 == 7:
+            out[i] = f[:-2] + struct.pack("<H", 3)
+    return out

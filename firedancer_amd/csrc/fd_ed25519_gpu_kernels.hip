@@ -2488,6 +2488,11 @@ extern "C" hipError_t fd_ed25519_gpu_launch_timed( uint64_t n, uint8_t const * b
   return fd_ed25519_gpu_launch_back( n, blob, desc, w, out, stream, ev, mode, pool_min, quad_max, oct_max );
 }
 
+#ifndef FD_KERNELS_ID
+#define FD_KERNELS_ID "unknown"
+#endif
+extern "C" __attribute__((visibility("default"))) char const * fd_ed25519_gpu_kernels_id( void ) { return FD_KERNELS_ID; }
+
 /* diagnostics: fd_k_prep alone, writing each pending signature's k as
    [4][n] little-endian 64-bit words to kout and its prep status to w->status */
 extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * blob, uint64_t blob_sz,

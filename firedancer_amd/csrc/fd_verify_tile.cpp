@@ -752,6 +752,7 @@ FD_EXPORT void fd_verify_tile_lat_publish( void * ctx, unsigned long sig, void c
   fd_verify_tile_lat_t * h = (fd_verify_tile_lat_t *)ctx;
   unsigned long d = tspub >= tsorig ? tspub - tsorig : 0UL;
   unsigned long b = d / 1000UL;
+  if( b >= FD_VERIFY_TILE_LAT_BINS/2UL ) b = FD_VERIFY_TILE_LAT_BINS/2UL + (b - FD_VERIFY_TILE_LAT_BINS/2UL) / 64UL;
   if( b >= FD_VERIFY_TILE_LAT_BINS ) { b = FD_VERIFY_TILE_LAT_BINS - 1UL; h->over++; }
   h->bin[ b ]++;
   h->cnt++; h->sum_ns += d;

@@ -39,7 +39,13 @@ class TCache:
 
 
 GPU_MAX = 8   # FD_VERIFY_TILE_GPU_MAX
-LAT_BINS = 65536  # FD_VERIFY_TILE_LAT_BINS (1-us bins)
+LAT_BINS = 65536  # FD_VERIFY_TILE_LAT_BINS (1-us bins to 32.768 ms, then 64-us bins to 2.13 s)
+
+
+def lat_bin_ms(b):
+    """centre of native latency bin b, ms (fd_verify_tile_lat_publish)"""
+    h = LAT_BINS // 2
+    return (b + 0.5) * 1e-3 if b < h else (h + (b - h) * 64 + 32) * 1e-3
 
 
 class LatHist:
@@ -68,10 +74,10 @@ class LatHist:
         c = np.cumsum(bins)
 
         def pct(q):
-            return float(np.searchsorted(c, q * cnt) + 0.5) * 1e-3   # ms, bin centre
+            return float(lat_bin_ms(int(np.searchsorted(c, q * cnt))))   # ms, bin centre
 
         return {"count": cnt, "mean_ms": sum_ns / cnt * 1e-6, "p50_ms": pct(0.5), "p99_ms": pct(0.99),
-                "p999_ms": pct(0.999), "max_ms": max_ns * 1e-6, "over_65ms": over}
+                "p999_ms": pct(0.999), "max_ms": max_ns * 1e-6, "over_2s": over}
 
 
 class VerifyTile:

@@ -370,6 +370,12 @@ int fd_ed25519_gpu_dev_stats_end  ( fd_ed25519_gpu_t * gpu, float * kernel_ms_su
    device, shared by every engine on it. */
 int fd_ed25519_gpu_dsm_clock( fd_ed25519_gpu_t * gpu, int clear, unsigned long long * out );
 
+/* Build id of the library's device code (16 hex digits: a hash of the
+   kernel sources and compile flags, firedancer_amd/Makefile KID).
+   Measurements of the kernels (profiles/pmc_traffic.json) name it;
+   host-only rebuilds keep it. */
+char const * fd_ed25519_gpu_kernels_id( void );
+
 /* Device the engine runs on; last HIP error string (diagnostics). */
 int          fd_ed25519_gpu_device( fd_ed25519_gpu_t const * gpu );
 char const * fd_ed25519_gpu_last_error( void );

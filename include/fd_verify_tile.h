@@ -173,8 +173,9 @@ fd_verify_tile_rx_burst_now( fd_verify_tile_t *    tile,
                              unsigned long         n );
 
 /* Diagnostics: a publish callback (ctx = fd_verify_tile_lat_t *) that
-   records each published frag's tspub - tsorig in 1-us bins (the last
-   bin and `over` catch >= 65.535 ms). */
+   records each published frag's tspub - tsorig: bin b < 32768 holds
+   b us, bin 32768 + j holds 32.768 ms + [64 j, 64 j + 64) us (up to
+   2.13 s; the last bin and `over` catch the rest). */
 #define FD_VERIFY_TILE_LAT_BINS (65536UL)
 typedef struct {
   unsigned long cnt, sum_ns, max_ns, over;

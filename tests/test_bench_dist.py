@@ -44,3 +44,24 @@ def test_bench_single_rank_dry():
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["n_gpus"] == 1 and res["value"] > 0
+
+
+def test_traffic_summary_held_to_the_kernels_build(tmp_path):
+    """roofline.traffic only from a PMC summary of the loaded device code
+    (fd_ed25519_gpu_kernels_id) at this launch size; the committed summary
+    must be of the committed kernels"""
+    sys.path.insert(0, ROOT)
+    import bench
+    import firedancer_amd as fa
+    kid = fa.kernels_id()
+    assert len(kid) == 16 and kid != "unknown"
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"kernels_id": kid, "sigs_per_launch": 1024,
+                             "kernels": {"fd_k_dsm_pool": {"hbm_bytes_per_launch": 5.0}}}))
+    assert bench.load_traffic(str(p), 1024, "fd_k_dsm_pool", kid) == (5.0, "current")
+    v, st = bench.load_traffic(str(p), 1024, "fd_k_dsm_pool", "0" * 16)
+    assert v is None and st.startswith("stale")
+    v, st = bench.load_traffic(str(p), 2048, "fd_k_dsm_pool", kid)
+    assert v is None
+    committed = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    assert committed.get("kernels_id") == kid, "profiles/pmc_traffic.json is not of these kernels: rerun tools/gpu.sh pmcthr"

@@ -37,6 +37,8 @@ def test_c5_record_window_equals_reference(ref):
     b = corpus.solana_txns(chk["sigs"], seed=chk["seed"], sig_dist=[1 / 12] * 12, nthreads=min(16, os.cpu_count() or 8))
     starts = sorted({int(d["sig_off"]) // corpus.TXN_MTU * corpus.TXN_MTU for d in b.desc})
     frags = [txn.frag(bytes(b.blob[s:s + corpus.TXN_MTU])) for s in starts[:chk["frags"]]]
+    if chk.get("edits") == "corpus.c5_check_edits":
+        frags = corpus.c5_check_edits(frags)
     # the reference's per-frag semantics, keeping each published frag's index
     r = _ref_tc(ref, 16, 64)
     cand, descs, owners, blob, off = [], [], [], [], 0
@@ -66,6 +68,8 @@ def test_c5_record_window_equals_reference(ref):
     pub = np.array([c for c, g in zip(cand, ok) if g], np.uint64)
     assert len(pub) == chk["published"]
     assert hashlib.sha256(pub.tobytes()).hexdigest() == chk["pub_ctl_sha256"]
+    if chk.get("edits"):      # the edits reach every branch of the per-frag semantics
+        assert ha > 0 and bad > 0 and (~ok).sum() > 0
     d = chk["diag"]
     assert d["PUB_CNT"] == len(pub) and d["SV_FILT_CNT"] == int((~ok).sum())
     assert d["HA_FILT_CNT"] == ha and d["BAD_CNT"] == bad and d["SIG_CNT"] == len(codes)

@@ -102,15 +102,22 @@ def run(a):
     if a.check_window:
         # the sample window: a collecting tile of the same layout over the
         # first W frags (fresh tcache), published ctl (= frag index) in order
+        # (with corpus.c5_check_edits: rejected signatures, dedup hits and
+        # frags that do not parse among them)
         W = min(a.check_window, len(frags))
+        cf = corpus.c5_check_edits(frags[:W])
+        cbase = np.frombuffer(b"".join(cf), np.uint8).copy()
+        csz = np.array([len(f) for f in cf], np.uint32)
+        coff = np.concatenate([[0], np.cumsum(csz)[:-1]]).astype(np.uint64)
         ct = VerifyTile(engs if a.multi else engs[0], batch_sigs=a.batch, collect=True,
-                        region=base if a.inplace else None)
-        ct.rx_burst(base, off[:W], sz[:W], ctl=np.arange(W, dtype=np.uint64))
+                        region=cbase if a.inplace else None)
+        ct.rx_burst(cbase, coff, csz, ctl=np.arange(W, dtype=np.uint64))
         ct.service(flush=True)
         pub_ctl = np.array([p[2] for p in ct.published], np.uint64)
         import hashlib
         check = {"frags": W, "published": int(len(pub_ctl)), "pub_ctl_sha256": hashlib.sha256(pub_ctl.tobytes()).hexdigest(),
-                 "diag": {k: int(v) for k, v in ct.diag().items()}, "seed": 77 + rank, "sigs": a.sigs}
+                 "diag": {k: int(v) for k, v in ct.diag().items()}, "seed": 77 + rank, "sigs": a.sigs,
+                 "edits": "corpus.c5_check_edits"}
         ct.close()
     if a.multi:       # one tile, every engine behind its feeder
         lats = [LatHist()] if a.latency else [None]

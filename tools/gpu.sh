@@ -15,7 +15,7 @@
 #     pmcthr                  PMC passes over the throughput step (VALU, FETCH, WRITE)
 #     pmcsq=lib               the SQ pass alone over the throughput step on a variant library
 #     ringpaced[=args]        tools/ring_paced.py (open-loop 4,096-batch ring)
-#     py=script[,args]        any tools/*.py under a 300 s limit
+#     py=script[,args]        any tools/*.py under a 300 s limit (appends gpurun_out/<script>.out)
 #     libpy=lib:script[,args] the same with FD_ED25519_LIB=lib (a variant library)
 #     native=prog[,args]      tools/build/prog (tools/Makefile) under a 300 s limit
 set -o pipefail
@@ -72,7 +72,7 @@ for step in "$@"; do
       mkdir -p gpurun_out/pmc
       B=("$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-latency)
       lib=$R/firedancer_amd/libfd_ed25519_gpu.so
-      sha256sum "$lib" | cut -c1-16 > gpurun_out/pmc/lib.sha16
+      python3 -c "import firedancer_amd as fa; print(fa.kernels_id())" > gpurun_out/pmc/kernels.id || exit 1
       pmc thr_p1 "$lib" $P1 -- "${B[@]}" || exit 1
       pmc thr_fetch "$lib" FETCH_SIZE -- "${B[@]}" || exit 1
       pmc thr_write "$lib" WRITE_SIZE -- "${B[@]}" || exit 1 ;;
@@ -87,7 +87,7 @@ for step in "$@"; do
     py)
       script=${arg%%,*}; rest=""; [[ $arg == *,* ]] && rest=${arg#*,}
       out=gpurun_out/$(basename "$script" .py)
-      timeout -k 10 300 python3 -u "tools/$script" ${rest//,/ } > "$out.out" 2> "$out.err" \
+      timeout -k 10 300 python3 -u "tools/$script" ${rest//,/ } >> "$out.out" 2>> "$out.err" \
         || { echo "PY $script FAILED"; tail -20 "$out.err"; exit 1; }
       tail -20 "$out.out" ;;
     libpy)

@@ -13,9 +13,9 @@ Per kernel, averaged over its dispatches:
     (wave-instructions per SIMD-cycle), effective clock, wait fractions.
 
 usage: pmc_summary.py <gpurun_out/pmc> <out.json> <sigs_per_launch>
-The library the passes ran is named by <gpurun_out/pmc>/lib.sha16 (written
-by tools/gpu.sh pmcthr); bench.py uses the summary only while that hash
-equals the loaded library's.
+The device code the passes ran is named by <gpurun_out/pmc>/kernels.id
+(fd_ed25519_gpu_kernels_id, written by tools/gpu.sh pmcthr); bench.py uses
+the summary only while that id equals the loaded library's.
 """
 import collections
 import csv
@@ -43,9 +43,9 @@ def load(d):
 def main():
     src, dst, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
     raw = load(src)
-    shaf = os.path.join(src, "lib.sha16")
-    sha = open(shaf).read().split()[0] if os.path.exists(shaf) else None
-    out = {"sigs_per_launch": n, "lib_sha16": sha, "source": "tools/gpu.sh pmcthr (rocprofv3 --pmc, one pass per group)",
+    kf = os.path.join(src, "kernels.id")
+    kid = open(kf).read().split()[0] if os.path.exists(kf) else None
+    out = {"sigs_per_launch": n, "kernels_id": kid, "source": "tools/gpu.sh pmcthr (rocprofv3 --pmc, one pass per group)",
            "correction": "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halves 16 B/lane reads)",
            "kernels": {}}
     for k, c in sorted(raw.items()):

@@ -55,6 +55,20 @@ def main():
     done = np.sort(st["t_done_ns"].astype(np.int64))
     gaps = np.diff(done) * 1e-6
     out["completion_gap_ms"] = {"p50": float(np.percentile(gaps, 50)), "p99": float(np.percentile(gaps, 99)), "max": float(gaps.max())}
+    # around the worst job: per 5 ms of its scheduled time, jobs completed,
+    # the ring's carried rate and the mean submit -> done (a slower ring or
+    # a host stall shows here)
+    t0 = int(st["t_sched_ns"][0])
+    ts = (st["t_sched_ns"].astype(np.int64) - t0) * 1e-6
+    td = (st["t_done_ns"].astype(np.int64) - t0) * 1e-6
+    w = int(np.argmax(tot))
+    lo = max(0.0, ts[w] - 60.0)
+    rows = []
+    for b0 in np.arange(lo, ts[w] + 20.0, 5.0):
+        m = (td >= b0) & (td < b0 + 5.0)
+        rows.append([round(float(b0 - ts[w]), 1), int(m.sum()), round(float(m.sum()) * B / 5e-3 / 1e6, 2),
+                     round(float(comp["submit_to_done"][m].mean()), 3) if m.any() else None])
+    out["around_worst"] = {"cols": ["t_rel_ms", "done", "carried_Mps", "submit_to_done_ms"], "rows": rows}
     print(json.dumps(out), flush=True)
 
 
