@@ -326,6 +326,17 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
 struct fd_sha2_ring { uint64_t w[2][FD_SHA2_CW][64]; };   /* 8 KiB, lane-contiguous (no bank conflicts) */
 typedef __attribute__((address_space(3))) fd_sha2_ring fd_sha2_lds_ring;
 
+/* FD_SHA2_WK 1: the schedule wave hands over W[t] + K[t] (the constant is
+   an immediate there, its loop being unrolled); the round wave then has no
+   scalar load of the chunk's constants -- and no wait on it after every
+   barrier -- and one 64-bit add less per round (276 -> 264 instructions
+   per 8-round chunk).  Measured on one signature (tools/oct_clock.py,
+   profiles/r05_sha2_wk_ab.jsonl): call p50 0.3565 ms (0) vs 0.3582 (1) --
+   the schedule wave, one add more per word, paces the pair as much as the
+   round wave does -- so 0, W[t] only, stays the default. */
+#ifndef FD_SHA2_WK
+#define FD_SHA2_WK 0
+#endif
 #define FD_SHA_ROUND_W(wj,kt) do {                                                 \
     uint64_t hkw = fd_opaque64u( h + (kt) + (wj) );                             \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
@@ -351,8 +362,13 @@ FD_DEV void fd_sha2_rounds( uint64_t (&st)[8], fd_sha2_lds_ring * ring, uint32_t
       uint64_t W[FD_SHA2_CW];
 #pragma unroll
       for( int j=0; j<FD_SHA2_CW; j++ ) W[j] = ring->w[k & 1u][j][lane];
+#if FD_SHA2_WK
+#pragma unroll
+      for( int j=0; j<FD_SHA2_CW; j++ ) FD_SHA_ROUND_W( W[j], 0ULL );
+#else
 #pragma unroll
       for( int j=0; j<FD_SHA2_CW; j++ ) FD_SHA_ROUND_W( W[j], fd_gpu_sha512_k[FD_SHA2_CW*ch + j] );
+#endif
       k++;
     }
     bool upd = blk < nblk;
@@ -411,7 +427,7 @@ FD_DEV void fd_sha2_schedule( fd_sha2_lds_ring * ring, fd_lds_u8 * stage, bool l
           uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
           w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
         }
-        ring->w[k & 1u][j][lane] = w[t&15];
+        ring->w[k & 1u][j][lane] = FD_SHA2_WK ? w[t&15] + fd_gpu_sha512_k[t] : w[t&15];
       }
       __syncthreads();
       k++;
@@ -480,7 +496,7 @@ FD_DEV void fd_sha2_schedule_direct( fd_sha2_lds_ring * ring, bool live, uint8_t
           uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
           w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
         }
-        ring->w[k & 1u][j][lane] = w[t&15];
+        ring->w[k & 1u][j][lane] = FD_SHA2_WK ? w[t&15] + fd_gpu_sha512_k[t] : w[t&15];
       }
       __syncthreads();
       k++;
