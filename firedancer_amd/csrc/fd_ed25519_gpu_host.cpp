@@ -378,23 +378,25 @@ static hipError_t fd_reg_release( void * host );
 extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
   if( !g ) return;
   hipSetDevice( g->device );
-  /* drain every stream, each wait bounded: if the device is wedged the
-     engine's memory is leaked rather than freed under a running kernel */
-  long to = fd_timeout( g );
-  for( int s=0; s<g->depth; s++ ) {
-    hipStream_t sts[2] = { g->slot[s].stream, g->slot[s].mstream };
-    for( int k=0; k<2; k++ )
-      if( sts[k] && fd_wait_query( fd_stream_query, (void *)sts[k], FD_POLL_SPIN_NS, to ) != 1 ) {
-        snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
-        return;
-      }
-  }
-  hipStream_t dsts[2] = { g->dev_sf, g->dev_sb };
-  for( int k=0; k<2; k++ )
-    if( dsts[k] && fd_wait_query( fd_stream_query, (void *)dsts[k], FD_POLL_SPIN_NS, to ) != 1 ) {
+  /* drain every stream, all waits under ONE deadline (the engine timeout
+     for the whole drain, not per stream: 2 x depth + 2 streams at 10 s
+     each made a wedged teardown take minutes): if the device is wedged
+     the engine's memory is leaked rather than freed under a running
+     kernel */
+  long to = fd_timeout( g ), t0 = fd_now_ns();
+  hipStream_t sts[2*FD_GPU_DEPTH_MAX + 2];
+  int ns = 0;
+  for( int s=0; s<g->depth; s++ ) { sts[ns++] = g->slot[s].stream; sts[ns++] = g->slot[s].mstream; }
+  sts[ns++] = g->dev_sf; sts[ns++] = g->dev_sb;
+  for( int k=0; k<ns; k++ ) {
+    if( !sts[k] ) continue;
+    long left = to < 0 ? -1L : to - (fd_now_ns() - t0);
+    if( to >= 0 && left < 0 ) left = 0;
+    if( fd_wait_query( fd_stream_query, (void *)sts[k], FD_POLL_SPIN_NS, left ) != 1 ) {
       snprintf( fd_gpu_err, sizeof(fd_gpu_err), "fd_ed25519_gpu_delete: device %d did not drain; engine leaked", g->device );
       return;
     }
+  }
   for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p ) fd_reg_release( (void *)g->reg[k].p );
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
@@ -1085,7 +1087,13 @@ static void fd_default_engine_fini( void ) {
   std::lock_guard<std::mutex> guard( fd_default_lock );
   fd_ed25519_gpu_t * g = fd_default_gpu;
   fd_default_gpu = NULL;
-  if( g ) fd_ed25519_gpu_delete( g );
+  /* the process is ending: drain for at most 2 s, then leave the memory to
+     the process teardown rather than hold up exit */
+  if( g ) {
+    long to = fd_timeout( g );
+    if( to < 0 || to > 2000000000L ) __atomic_store_n( &g->timeout_ns, 2000000000L, __ATOMIC_RELAXED );
+    fd_ed25519_gpu_delete( g );
+  }
 }
 
 static fd_ed25519_gpu_t * fd_default_engine( void ) {

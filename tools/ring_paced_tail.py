@@ -20,6 +20,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def host_stats():
+    """CPU-quota throttling and preemption counters of this process's box
+    (cgroup v2 or v1 cpu.stat, /proc/pressure/cpu, involuntary context
+    switches): a host that stops the feeder thread shows here"""
+    import resource
+    out = {}
+    for f in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"):
+        try:
+            for line in open(f):
+                k, v = line.split()
+                out["cg_" + k] = int(v)
+            out["cg_file"] = f
+            break
+        except (OSError, ValueError):
+            pass
+    try:
+        for line in open("/proc/pressure/cpu"):
+            parts = line.split()
+            out["psi_" + parts[0] + "_total_us"] = int(parts[-1].split("=")[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out["nivcsw"] = ru.ru_nivcsw
+    out["nvcsw"] = ru.ru_nvcsw
+    return out
+
+
 def main():
     mps = float(sys.argv[1]) if len(sys.argv) > 1 else 36.0
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 4000
@@ -35,7 +62,10 @@ def main():
     B = bench.BATCH_SIGS
     starts = np.random.default_rng(7).permutation(len(ring) // B).astype(np.uint64) * B
     period = int(round(B / (mps * 1e6) * 1e9))
+    feeder.synth(ring.blob, ring.desc, B, starts, 400, 2 * depth, period)     # warm-up (first use of every slot and group)
+    h0 = host_stats()
     st = feeder.synth(ring.blob, ring.desc, B, starts, nb, 2 * depth, period)
+    h1 = host_stats()
     feeder.close()
     eng.close()
     st = st[2 * depth:]
@@ -69,6 +99,20 @@ def main():
         rows.append([round(float(b0 - ts[w]), 1), int(m.sum()), round(float(m.sum()) * B / 5e-3 / 1e6, 2),
                      round(float(comp["submit_to_done"][m].mean()), 3) if m.any() else None])
     out["around_worst"] = {"cols": ["t_rel_ms", "done", "carried_Mps", "submit_to_done_ms"], "rows": rows}
+    out["host_delta"] = {k: h1[k] - h0[k] for k in h1 if isinstance(h1[k], int) and k in h0}
+    out["host_cg_file"] = h1.get("cg_file")
+    # 2 ms windows of the run that completed less than half the offered rate
+    # while jobs were outstanding (a stall of the ring or of the host)
+    sched = np.sort(ts)
+    stalls = []
+    for b0 in np.arange(0.0, float(td.max()), 2.0):
+        done_b = int(((td >= b0) & (td < b0 + 2.0)).sum())
+        outstanding = int((ts < b0).sum()) - int((td < b0).sum())
+        if outstanding > 0 and done_b * B / 2e-3 < 0.5 * mps * 1e6:
+            stalls.append([round(float(b0), 1), done_b, outstanding])
+    out["slow_2ms_windows"] = stalls[:40]
+    out["slow_2ms_window_count"] = len(stalls)
+    del sched
     print(json.dumps(out), flush=True)
 
 
