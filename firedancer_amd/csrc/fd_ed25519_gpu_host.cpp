@@ -1067,12 +1067,17 @@ static unsigned long       fd_default_blob = 1UL << 26;
 static fd_ed25519_gpu_t * fd_default_engine( void );
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_default( void ) { return fd_default_engine(); }
 /* group-commit leaders of fd_ed25519_verify = the default engine's ring
-   depth (experiments: FD_ED25519_GPU_VQ_LEADERS, 1..FD_GPU_DEPTH_MAX) */
+   depth (experiments: FD_ED25519_GPU_VQ_LEADERS, 1..FD_GPU_DEPTH_MAX).
+   4: on the round-5 kernels (one box, profiles/r05_vq_leaders_ab.jsonl)
+   64 native threads 83.3-84.0 K calls/s at 3 leaders against 90.4 K at 4
+   (p99 1.08 ms) and 86.4 K at 5 (p99 1.22); 4 threads 8.8-9.0 K at p99
+   0.62-0.67 ms against 10.8 K at p99 0.40; one thread unchanged. */
+#define FD_VQ_LEADERS_DEFAULT 4
 static int fd_vq_leaders( void ) {
   static int n = 0;
   if( !n ) {
     char const * e = getenv( "FD_ED25519_GPU_VQ_LEADERS" );
-    int v = e ? atoi( e ) : FD_GPU_DEPTH_DEFAULT;
+    int v = e ? atoi( e ) : FD_VQ_LEADERS_DEFAULT;
     n = v < 1 ? 1 : v > FD_GPU_DEPTH_MAX ? FD_GPU_DEPTH_MAX : v;
   }
   return n;
