@@ -956,31 +956,25 @@ extern "C" hipError_t fd_ed25519_gpu_quad_acc( void * host, int clear ) {
    rows start 4 banks apart, so the step's byte reads of 16 signatures at
    one t hit 16 different banks; 16-byte aligned for ds_write_b128) */
 #define FD_QOPS_ROW (FD_OPS_MAX + 16)
-/* The quad step (FD_QUAD_STEP): 1 round 4's layout; 2 round 5's first
-   (C = V (.) rot V, own/partner operand forms, biased products,
-   fd_q2_kind_bits); 3 (default) the same layout with the per-step decode
-   read from an LDS table (fd_q3_entry), raw product limbs whose residual
-   masks fold into the operand / output masks, and xor-adds in the mix. */
-#ifndef FD_QUAD_STEP
-#define FD_QUAD_STEP 3
-#endif
-#if FD_QUAD_STEP >= 3
+/* The quad step (round 5): C = V (.) rot V, the
+   op's operand f from own / partner forms of C, h = f g, the output mix
+   over h's four lanes (lane layout in fd_ed25519_gpu_wnaf.h,
+   fd_q2_kind_bits), with the per-step decode read from an LDS table
+   (fd_q3_entry), raw product limbs whose residual masks fold into the
+   operand / output masks, and xor-adds in the mix.  Round 4's step (four
+   DPP-broadcast operands, four masked broadcasts in the mix) and round
+   5's first form are in the history (profiles/r05_quad_v2_ab.jsonl,
+   r05_quad_v3_ab.jsonl). */
 /* op rows from FD_QOPS_BASE on: a stream holds at most 2 x 51 digits
    (width-5 windows of two scalars below 2^253, fd_ed25519_gpu_wnaf.h), so
    it starts at FD_OPS_MAX - 256 - 102 = 154 or later; 400-byte rows (100
    dwords, 36 banks apart) keep the 16 rows' step reads on 16 banks */
 #define FD_QOPS_BASE 144
 #define FD_QOPS_ROWQ 400
-#else
-#define FD_QOPS_BASE 0
-#define FD_QOPS_ROWQ FD_QOPS_ROW
-#endif
 struct fd_quad_lds {
   int32_t tab[FD_QSIGS+1][8*FD_TAB_ENTRY];   /* Ai per signature, [FD_QSIGS] = Bi */
   uint8_t ops[FD_QSIGS][FD_QOPS_ROWQ];   /* signature-major, padded rows (from t = FD_QOPS_BASE) */
-#if FD_QUAD_STEP >= 3
   int32_t dec[3*4*FD_Q3_DW];            /* fd_q3_entry per (op kind, lane) */
-#endif
 };
 FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   int4 * q = (int4 *)p;
@@ -1093,13 +1087,11 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
   fd_lat_stage<FD_QSIGS, 8*FD_TAB_ENTRY, FD_QOPS_ROWQ, FD_QOPS_BASE>( ops, sig0, n, t0, L.ops, L.tab[FD_QSIGS], fd_bi_quad{} );
-#if FD_QUAD_STEP >= 3
   /* the step decode table: 12 entries x FD_Q3_DW dwords, 6 per lane */
   for( uint32_t k = threadIdx.x & 63u; k < 3u*4u*FD_Q3_DW; k += 64u ) {
     uint32_t const e = k / FD_Q3_DW, dw = k % FD_Q3_DW;
     L.dec[k] = (int32_t)fd_q3_entry( e & 3u, (int)(e >> 2), (int)dw );
   }
-#endif
 
   /* per-lane constant masks */
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
@@ -1135,21 +1127,15 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   }
   __syncthreads();
 
-  /* main loop: the uniform kernel's step (see fd_k_dsm) with lane q of
-     the quad forming product q of the p1p1 -> p3 conversion
-     [Z,Y,X,T] = [t2 t3, t1 t2, t0 t3, t0 t1] and then product q of the op
-     (P, Q, R, S), followed by the op's output mix */
+  /* main loop: per step two products per lane.  C = V (.) rot V (lane q
+     multiplies its p1p1 component t_q by t_{q+1}, so C = [T, Y, Z, X],
+     the p1p1 -> p3 conversion); f = a C + b C' (C' the partner lane's C,
+     quad_perm 3,3,2,1; a, b per lane and op kind); g = the table entry
+     (add) or f (doubling, 2f on lane 2); h = f g = [S, P, Q, R]; the
+     state for the next step is the op's output mix of h's lanes */
   fd_fe_set( vt, q ? 1 : 0 );
   uint32_t const tab_bi = (uint32_t)(L.tab[FD_QSIGS] - tab_s);   /* int32s from this signature's Ai to Bi */
-#if FD_QUAD_STEP == 2
-  /* this lane's decode words for D, positive-digit add, negative-digit add
-     (fd_q2_kind_bits: the step's lane layout, masks and bias constants) */
-  uint32_t const kw0 = fd_q2_kind_bits( q, 0, 0 ), kw1 = fd_q2_kind_bits( q, 1, 0 ), kw2 = fd_q2_kind_bits( q, 1, 1 );
-#elif FD_QUAD_STEP >= 3
   int32_t const * const dec_q = L.dec + q*FD_Q3_DW;   /* + kind * 4 * FD_Q3_DW */
-#else
-  uint64_t const okw = fd_op_kind_word( q );
-#endif
   __builtin_amdgcn_wave_barrier();
   unsigned long long qs_c0 = __builtin_amdgcn_s_memtime(), qs_r0 = __builtin_amdgcn_s_memrealtime();
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
@@ -1158,11 +1144,6 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
        any other row's bytes only steer lanes whose result is discarded
        (code != FD_ST_PENDING), with table indices bounded by the masks */
     int op = (int)L.ops[ls][t - FD_QOPS_BASE];
-#if FD_QUAD_STEP == 2
-    uint32_t const madd = fd_ok_mask( (uint32_t)op, 7 ), mneg = fd_ok_mask( (uint32_t)op, 5 );
-    uint32_t const kd = fd_sel( madd, fd_sel( mneg, kw2, kw1 ), kw0 );
-    uint32_t idx = fd_ok_bits( kd, FD_Q2_IDX, 2 );
-#elif FD_QUAD_STEP >= 3
     /* this lane's decode entry for the op's kind (D 0, +add 1, -add 2) */
     uint32_t const kind = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);
     int32_t D[FD_Q3_DW];
@@ -1172,32 +1153,20 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
       for( int j=0; j<FD_Q3_DW/4; j++ ) { int4 x = de[j]; D[4*j] = x.x; D[4*j+1] = x.y; D[4*j+2] = x.z; D[4*j+3] = x.w; }
     }
     uint32_t const madd = (uint32_t)D[FD_Q3_MADD];
-    uint32_t idx = 0;   /* the entry lane's offset comes with the entry */
-#else
-    uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
-    uint32_t add = fd_ok_mask( kd, FD_OK_QS );
-    /* table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3 */
-    uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
-#endif
     int32_t E[10];
     {
       /* Bi (op bit 6) or this signature's Ai: the row offset by arithmetic,
          not a compare and select (a VALU-written SGPR mask costs wait states) */
-#if FD_QUAD_STEP >= 3
+      /* (the table entry lane's offset comes with the decode entry) */
       int32_t const * ent = tab_s + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_TAB_ENTRY + (uint32_t)D[FD_Q3_IDX];
-      (void)idx;
-#else
-      int32_t const * ent = tab_s + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_TAB_ENTRY + idx*FD_TAB_LANE;
-#endif
       int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1], ec = ((int4 const *)ent)[2];
       E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x; E[5] = eb.y; E[6] = eb.z; E[7] = eb.w; E[8] = ec.x; E[9] = ec.y;
     }
 
-#if FD_QUAD_STEP >= 3
-    /* the step of FD_QUAD_STEP 2 (below) on raw product limbs: each limb's
-       residual mask is folded into the mask that selects it (the entry's
-       E / O variants; limbs 1 and 5 arrive materialized, class X) and its
-       bias into kf / K of its class */
+    /* on raw product limbs (fd_fe_mul_raw): each limb's residual mask is
+       folded into the mask that selects it (the entry's E / O variants;
+       limbs 1 and 5 arrive materialized, class X) and its carry bias into
+       kf / K of its class */
     fe Cr;
     fd_fe_qperm<FD_QP(1,2,3,0)>( g, vt );
     fd_fe_mul_raw( Cr, vt, g );
@@ -1229,105 +1198,6 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
       uint32_t const x1 = fd_xad( c, sR, (uint32_t)D[kc] ), x2 = fd_xad( d, sS, a );
       vt.v[k] = (int32_t)((b << qs) + x1 + x2);
     }
-#elif FD_QUAD_STEP == 2
-    /* C = V (.) rot(V): lane q forms t_q t_{q+1}, so C = [T, Y, Z, X] and
-       only g needs a quad move (X = t3 t0 takes its operands in the other
-       order than the reference's t0 t3: the same exact column sums, as no
-       operand pre-scale wraps at the DSM's limb sizes, tests/test_fe_host.py);
-       limbs come out biased, the bias folded into f's constant below */
-    fe Cb;
-    fd_fe_qperm<FD_QP(1,2,3,0)>( g, vt );
-    fd_fe_mul_b( Cb, vt, g );
-
-    /* f = a C + b C' (C' from lane 3,3,2,1 by a DPP-folded v_and):
-       q0 D: X, A: T; q1 X+Y; q2 Z; q3 D: Y, A: Y-X.  g: E on an add, f on a
-       doubling (q2: 2Z).  h = f g = [S, P, Q, R] */
-    uint32_t const mA = fd_ok_mask( kd, FD_Q2_MA ), sA = fd_ok_mask( kd, FD_Q2_SA );
-    uint32_t const mBv = (uint32_t)fd_opaque( (int32_t)fd_ok_mask( kd, FD_Q2_MB ) );
-    uint32_t const kfe = kd & 0xFF000001u;                                     /* sA - (a+b) 2^25 */
-    uint32_t const kfo = (uint32_t)((int32_t)(kd & 0xFF000000u) >> 1) + (kd & 1u);  /* sA - (a+b) 2^24 */
-    uint32_t const gs = fd_ok_bits( kd, FD_Q2_GS, 1 );
-#pragma unroll
-    for( int k=0; k<10; k++ ) {
-      uint32_t const p = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,2,1)>( Cb.v[k] ) & mBv) );
-      uint32_t const fk = fd_andxor( (uint32_t)Cb.v[k], mA, sA ) + p + ((k & 1) ? kfo : kfe);
-      f.v[k] = (int32_t)fk;
-      g.v[k] = (int32_t)fd_sel( madd, (uint32_t)E[k], fk << gs );
-    }
-    fe h; fd_fe_mul_b( h, f, g );
-
-    /* V' = cP P + cQ Q + cR R + cS S from h = [S, P, Q, R] (the masks of
-       fd_op_kind_bits per output lane), the biases of h folded into K */
-    uint32_t const mP = fd_ok_mask( kd, FD_Q2_MP ), mQ = fd_ok_mask( kd, FD_Q2_MQ ), qs = madd & 1u;
-    uint32_t const mR = fd_ok_mask( kd, FD_Q2_MR ), sR = fd_ok_mask( kd, FD_Q2_SR );
-    uint32_t const mS = fd_ok_mask( kd, FD_Q2_MS ), sS = fd_ok_mask( kd, FD_Q2_SS );
-    uint32_t const cadd = fd_ok_bits( kd, FD_Q2_CADD, 2 ), sc = fd_ok_bits( kd, FD_Q2_SUMC, 8 );
-    uint32_t const Ke = (sc << 25) + cadd, Ko = (sc << 24) + cadd;
-    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
-    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
-#pragma unroll
-    for( int k=0; k<10; k++ ) {
-      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( h.v[k] ) & mPv) );
-      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( h.v[k] ) & mQv) );
-      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( h.v[k] ) & mRv) );
-      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( h.v[k] ) & mSv) );
-      vt.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + ((k & 1) ? Ko : Ke));
-    }
-#else
-    fe C;
-    fd_fe_qperm<FD_QP(2,1,0,0)>( f, vt ); fd_fe_qperm<FD_QP(3,2,3,1)>( g, vt );
-    FD_QMUL( C, f, g );
-
-    /* f: q0 X+Y, q1 Z, q2 Y (A: Y-X), q3 X (A: T); g: D f (q1 2Z), A E */
-    fe u, w;
-    fd_fe_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fe_qperm<FD_QP(2,2,2,2)>( w, C );
-    uint32_t mW = fd_ok_mask( kd, FD_OK_MW ), mT = fd_ok_mask( kd, FD_OK_MT );
-    uint32_t gs = fd_ok_bits( kd, FD_OK_GS, 1 );
-    /* u + fd_qterm( w, mW, mq2 ) as u + ((w & mW) ^ mq2) + (mq2 & 1): one
-       v_bitop3 and one v_add3 per limb (-s == s & 1 for a mask s; LLVM
-       otherwise selects between w & mW and its negation) */
-    uint32_t const s2b = (uint32_t)fd_opaque( (int32_t)(mq2 & 1u) );
-#pragma unroll
-    for( int k=0; k<10; k++ ) {
-      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_andxor( (uint32_t)w.v[k], mW, mq2 ) + s2b );
-      f.v[k] = (int32_t)fk;
-      g.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
-    }
-    fe h; FD_QMUL( h, f, g );
-
-    /* out = cP P + cQ Q + cR R + cS S, per lane and op kind:
-         q0 D: P-R-S      A: P-R
-         q1 D: R+S        A: P+R
-         q2 D: R-S        A: 2Q-S (positive digit: 2Q+S)
-         q3 D: Q-R+S      A: 2Q+S (positive digit: 2Q-S) */
-    uint32_t mP = fd_ok_mask( kd, FD_OK_MP ), mQ = fd_ok_mask( kd, FD_OK_MQ ), qs = fd_ok_bits( kd, FD_OK_QS, 1 );
-    uint32_t mR = fd_ok_mask( kd, FD_OK_MR ), sR = fd_ok_mask( kd, FD_OK_SR );
-    uint32_t mS = fd_ok_mask( kd, FD_OK_MS ), sS = fd_ok_mask( kd, FD_OK_SS );
-    uint32_t cadd = fd_ok_bits( kd, FD_OK_CADD, 2 );
-#if FD_QUAD_DPP_AND
-    /* each broadcast masked by a v_and_b32 with the quad move folded in
-       (VOP2 DPP); the barriers keep LLVM from fusing and + xor into a
-       v_bitop3 (VOP3, which takes no DPP operand on gfx950) */
-    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
-    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
-#pragma unroll
-    for( int k=0; k<10; k++ ) {
-      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( h.v[k] ) & mPv) );
-      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( h.v[k] ) & mQv) );
-      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( h.v[k] ) & mRv) );
-      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( h.v[k] ) & mSv) );
-      vt.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + cadd);
-    }
-#else
-    fe P, Q, R, S;
-    fd_fe_qperm<FD_QP(0,0,0,0)>( P, h ); fd_fe_qperm<FD_QP(1,1,1,1)>( Q, h );
-    fd_fe_qperm<FD_QP(2,2,2,2)>( R, h ); fd_fe_qperm<FD_QP(3,3,3,3)>( S, h );
-#pragma unroll
-    for( int k=0; k<10; k++ )
-      vt.v[k] = (int32_t)(((uint32_t)P.v[k] & mP) + (((uint32_t)Q.v[k] & mQ) << qs)
-                          + (((uint32_t)R.v[k] & mR) ^ sR) + (((uint32_t)S.v[k] & mS) ^ sS) + cadd);
-#endif
-#endif
   }
 
 #ifdef FD_QUAD_STAMPS
@@ -1624,20 +1494,13 @@ struct fd_bi_oct {
   __device__ __forceinline__ int src( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_TAB_ENTRY + l*FD_TAB_LANE + limb; }
   __device__ __forceinline__ int dst( int k ) const { int e = k / 40, l = (k / 10) % 4, limb = k % 10; return e*FD_OTAB_ENTRY + l*FD_OTAB_LANE + (limb < 5 ? limb : limb + 3); }
 };
-/* The oct step (FD_OCT_STEP): 1 round 4's (the quad's round-4 layout on
-   half elements); 3 (default) the quad's FD_QUAD_STEP 2 layout on half
-   elements (C = V (.) rot V, own/partner operand forms, biased products)
-   with its decode read from an LDS table (fd_o3_entry) and xor-adds in
-   the mix */
-#ifndef FD_OCT_STEP
-#define FD_OCT_STEP 3
-#endif
+/* The oct step (round 5): the quad's step layout on half elements
+   (C = V (.) rot V, own/partner operand forms, biased products) with its
+   decode read from an LDS table (fd_o3_entry) and xor-adds in the mix */
 struct fd_oct_lds {
   int32_t tab[FD_OSIGS+1][8*FD_OTAB_ENTRY];   /* Ai per signature, [FD_OSIGS] = Bi */
   uint8_t ops[FD_OSIGS][FD_QOPS_ROW];
-#if FD_OCT_STEP >= 3
   int32_t dec[3*4*2*FD_O3_DW];              /* fd_o3_entry per (op kind, lane q, half h) */
-#endif
 };
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -1667,12 +1530,10 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   /* wave-uniform, in an SGPR: the step loop is then counted by the scalar unit */
   int t0 = __builtin_amdgcn_readfirstlane( fd_wave_min( start ) );
   fd_lat_stage<FD_OSIGS, 8*4*10, FD_QOPS_ROW, 0>( ops, sig0, n, t0, L.ops, L.tab[FD_OSIGS], fd_bi_oct{} );
-#if FD_OCT_STEP >= 3
   for( uint32_t k = threadIdx.x & 63u; k < 3u*4u*2u*FD_O3_DW; k += 64u ) {
     uint32_t const e = k / FD_O3_DW, dw = k % FD_O3_DW;   /* e = (kind*4 + q)*2 + h */
     L.dec[k] = (int32_t)fd_o3_entry( (e >> 1) & 3u, e & 1u, (int)(e >> 3), (int)dw, FD_OTAB_LANE );
   }
-#endif
 
   uint32_t const mq0 = q==0u ? ~0u : 0u, mq1 = q==1u ? ~0u : 0u, mq2 = q==2u ? ~0u : 0u, mq3 = q==3u ? ~0u : 0u;
   uint32_t const m12 = mq1 | mq2, m03 = mq0 | mq3, s02 = mq0 | mq2;
@@ -1708,9 +1569,8 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
   }
   __syncthreads();
 
-#if FD_OCT_STEP >= 3
-  /* main loop: the quad's step (FD_QUAD_STEP 2 layout) on half field
-     elements, its decode from the LDS table */
+  /* main loop: the quad's step layout on half field elements, its decode
+     from the LDS table */
   int32_t const * const dec_qh = L.dec + (q*2u + h)*FD_O3_DW;   /* + kind * 8 * FD_O3_DW */
   uint32_t const tab_bi = (uint32_t)(L.tab[FD_OSIGS] - L.tab[ls]);   /* int32s from this signature's Ai to Bi */
   fh s;
@@ -1764,62 +1624,6 @@ fd_k_dsm_oct( uint64_t n, int32_t const * __restrict__ status, int32_t const * _
       s.v[k] = (int32_t)((b << qs) + x1 + x2);
     }
   }
-#else
-  /* main loop: the quad's step on half field elements */
-  uint64_t const okw = fd_op_kind_word( q );
-  uint32_t const tab_bi = (uint32_t)(L.tab[FD_OSIGS] - L.tab[ls]);   /* int32s from this signature's Ai to Bi */
-  fh s;
-#pragma unroll
-  for( int k=0; k<5; k++ ) s.v[k] = 0;
-  s.v[0] = (int32_t)((q && !h) ? 1 : 0);
-  __builtin_amdgcn_wave_barrier();
-  unsigned long long os_c0 = __builtin_amdgcn_s_memtime(), os_r0 = __builtin_amdgcn_s_memrealtime();
-  for( int t=t0; t<FD_OPS_MAX; t++ ) {
-    int op = (int)L.ops[ls][t];
-    uint32_t const kd = fd_op_kind( okw, op );        /* this lane's decode of the op (fd_op_kind_word) */
-    uint32_t add = fd_ok_mask( kd, FD_OK_QS );
-    uint32_t idx = fd_ok_bits( kd, FD_OK_IDX, 2 );
-    int32_t E[5];
-    {
-      /* Bi (op bit 6) or this signature's Ai, as the quad */
-      int32_t const * ent = L.tab[ls] + ((uint32_t)(op >> 6) & 1u)*tab_bi + (op & 7)*FD_OTAB_ENTRY + idx*FD_OTAB_LANE + 8u*h;
-      int4 ea = ((int4 const *)ent)[0], eb = ((int4 const *)ent)[1];
-      E[0] = ea.x; E[1] = ea.y; E[2] = ea.z; E[3] = ea.w; E[4] = eb.x;
-    }
-
-    fh fo, go, C;
-    fd_fh_qperm<FD_QP(2,1,0,0)>( fo, s ); fd_fh_qperm<FD_QP(3,2,3,1)>( go, s );
-    fd_o_mul( C, fo, go, oc );
-
-    fh u, w;
-    fd_fh_qperm<FD_QP(1,0,1,2)>( u, C ); fd_fh_qperm<FD_QP(2,2,2,2)>( w, C );
-    uint32_t mW = fd_ok_mask( kd, FD_OK_MW ), mT = fd_ok_mask( kd, FD_OK_MT );
-    uint32_t gs = fd_ok_bits( kd, FD_OK_GS, 1 );
-    uint32_t const s2b = (uint32_t)fd_opaque( (int32_t)(mq2 & 1u) );
-#pragma unroll
-    for( int k=0; k<5; k++ ) {
-      uint32_t fk = fd_sel( mT, (uint32_t)C.v[k], (uint32_t)u.v[k] + fd_andxor( (uint32_t)w.v[k], mW, mq2 ) + s2b );
-      fo.v[k] = (int32_t)fk;
-      go.v[k] = (int32_t)fd_sel( add, (uint32_t)E[k], fk << gs );
-    }
-    fh hq; fd_o_mul( hq, fo, go, oc );
-
-    uint32_t mP = fd_ok_mask( kd, FD_OK_MP ), mQ = fd_ok_mask( kd, FD_OK_MQ ), qs = fd_ok_bits( kd, FD_OK_QS, 1 );
-    uint32_t mR = fd_ok_mask( kd, FD_OK_MR ), sR = fd_ok_mask( kd, FD_OK_SR );
-    uint32_t mS = fd_ok_mask( kd, FD_OK_MS ), sS = fd_ok_mask( kd, FD_OK_SS );
-    uint32_t cadd = fd_ok_bits( kd, FD_OK_CADD, 2 );
-    uint32_t const mPv = (uint32_t)fd_opaque( (int32_t)mP ), mQv = (uint32_t)fd_opaque( (int32_t)mQ );
-    uint32_t const mRv = (uint32_t)fd_opaque( (int32_t)mR ), mSv = (uint32_t)fd_opaque( (int32_t)mS );
-#pragma unroll
-    for( int k=0; k<5; k++ ) {
-      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( hq.v[k] ) & mPv) );
-      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( hq.v[k] ) & mQv) );
-      uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( hq.v[k] ) & mRv) );
-      uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( hq.v[k] ) & mSv) );
-      s.v[k] = (int32_t)(a + (b << qs) + (c ^ sR) + (d ^ sS) + cadd);
-    }
-  }
-#endif
   fd_clk_add( 6, os_c0, os_r0, lane );
 
   /* the whole final state, then the quad's final p1p1 -> p2 and the limb

@@ -32,61 +32,6 @@ FD_DEV uint8_t fd_op_enc( int tbl, int d ) {
   return (uint8_t)(FD_OP_ADD | (tbl << 6) | ((d < 0) << 5) | (a >> 1));
 }
 
-/* Per-lane decode of an op for the lane-split DSMs (fd_k_dsm_quad /
-   fd_k_dsm_oct): what lane q of a signature's quad does in a step depends
-   only on q and the op's kind (0 D, 1 positive-digit add, 2 negative-digit
-   add).  A lane keeps one 64-bit word holding a 16-bit field per kind, so a
-   step's decode is a shift and one bit-field extract per value instead of
-   ~40 compares and selects (the masks below are the kernels' former
-   per-step expressions, tests/test_recode_host.py::test_op_kind_word):
-     bit  0  mW   q0 | q2 & add       (operand f: + W term)
-     bit  1  mT   q3 & add            (operand f: C itself)
-     bit  2  gs   q1 & !add           (operand g: f << 1)
-     bit  3  mP   q0 | q1 & add       (output mix: P)
-     bit  4  mQ   q3 | q2 & add       (output mix: Q)
-     bit  5  qs   add                 (output mix: Q << 1; also the add mask)
-     bit  6  mR   q0 | q1 | !add
-     bit  7  sR   q0 | q3 & !add      (output mix: R negated)
-     bit  8  mS   !((q0 | q1) & add)
-     bit  9  sS   q0 & !add | q2 & !pos | q3 & pos   (pos: add & !neg)
-     bits 10-11   cadd = sR + sS      (the negations' +1s)
-     bits 12-13   idx                 (table entry lane: q0 E2 (neg: E1), q1 E0, q2 E1 (neg: E2), q3 E3)
-   A D op is the byte 0 and an add has bit 7 set, so the kind is bit 7 +
-   bit 5 of the op byte. */
-#define FD_OK_MW   0
-#define FD_OK_MT   1
-#define FD_OK_GS   2
-#define FD_OK_MP   3
-#define FD_OK_MQ   4
-#define FD_OK_QS   5
-#define FD_OK_MR   6
-#define FD_OK_SR   7
-#define FD_OK_MS   8
-#define FD_OK_SS   9
-#define FD_OK_CADD 10
-#define FD_OK_IDX  12
-FD_DEV uint32_t fd_op_kind_bits( uint32_t q, int add, int neg ) {
-  uint32_t q0 = q == 0u, q1 = q == 1u, q2 = q == 2u, q3 = q == 3u;
-  uint32_t a = add ? 1u : 0u, na = 1u - a, pos = a & (neg ? 0u : 1u), npos = 1u - pos;
-  uint32_t sR = q0 | (q3 & na), sS = (q0 & na) | (q2 & npos) | (q3 & pos);
-  uint32_t idx = q0 ? (neg ? 1u : 2u) : q1 ? 0u : q2 ? (neg ? 2u : 1u) : 3u;
-  return ( q0 | (q2 & a) )            << FD_OK_MW
-       | ( q3 & a )                   << FD_OK_MT
-       | ( q1 & na )                  << FD_OK_GS
-       | ( q0 | (q1 & a) )            << FD_OK_MP
-       | ( q3 | (q2 & a) )            << FD_OK_MQ
-       | a                            << FD_OK_QS
-       | ( q0 | q1 | na )             << FD_OK_MR
-       | sR                           << FD_OK_SR
-       | ( 1u - ((q0 | q1) & a) )     << FD_OK_MS
-       | sS                           << FD_OK_SS
-       | ( sR + sS )                  << FD_OK_CADD
-       | idx                          << FD_OK_IDX;
-}
-FD_DEV uint64_t fd_op_kind_word( uint32_t q ) {
-  return (uint64_t)fd_op_kind_bits( q, 0, 0 ) | ((uint64_t)fd_op_kind_bits( q, 1, 0 ) << 16)
-       | ((uint64_t)fd_op_kind_bits( q, 1, 1 ) << 32);
-}
 /* The quad DSM's step (fd_quad_body), per lane and op kind, as one
    32-bit word per kind (three per lane, selected by the op byte's bits 7
    and 5).  Lane layout of the step:
@@ -97,8 +42,8 @@ FD_DEV uint64_t fd_op_kind_word( uint32_t q ) {
        q3 D: Y (0,1), A: Y-X (-1,1);
      g = E (add) or f (D; q2: 2f), so h = [S, P, Q, R]:
        D [X^2, (X+Y)^2, 2Z^2, Y^2], A [TT, PP, ZZ, MM];
-     t_q = the output mix of fd_op_kind_bits (mP..sS, cadd) over those
-       source lanes.
+     t_q = the output mix mP P + mQ (Q << add) + (+-)mR R + (+-)mS S + cadd
+       over those source lanes (bits 6-13 below).
    C and h arrive with each limb's carry bias in (fd_fe_limbs_t<1>), so
    the two adds that already take a per-lane constant fold the biases out:
    f's constant kf = sA - (a+b) bias, the mix's K = cadd - (sum of its
@@ -130,7 +75,8 @@ FD_DEV uint32_t fd_q2_kind_bits( uint32_t q, int add, int neg ) {
   int fa = q0 ? (int)a : q1 ? 1 : q2 ? 1 : (add ? -1 : 0);
   int fb = q0 ? (int)na : q1 ? 1 : q2 ? 0 : 1;
   uint32_t idx = q0 ? 3u : q1 ? (neg ? 1u : 2u) : q2 ? 0u : (neg ? 2u : 1u);
-  /* the output mix (the same per output lane as fd_op_kind_bits) */
+  /* the output mix: which of h's lanes output lane q takes, with signs
+     (the reference's DBL_MIX / SUB_MIX / ADD_MIX lane permutations) */
   uint32_t mP = q0 | (q1 & a), mQ = q3 | (q2 & a), mR = q0 | q1 | na, mS = 1u - ((q0 | q1) & a);
   uint32_t sR = q0 | (q3 & na), sS = (q0 & na) | (q2 & npos) | (q3 & pos);
   int sumc = (int)mP + (int)mQ*(add ? 2 : 1) + (int)mR*(sR ? -1 : 1) + (int)mS*(sS ? -1 : 1);
@@ -213,7 +159,7 @@ FD_DEV uint32_t fd_q3_entry( uint32_t q, int kind, int dw ) {
   }
 }
 
-/* The eight-lane DSM's decode entries (fd_k_dsm_oct, FD_OCT_STEP 3): the
+/* The eight-lane DSM's decode entries (fd_k_dsm_oct): the
    quad's step layout (fd_q2_kind_bits) on half field elements, per (op
    kind, lane q, half h).  The oct's products come out biased
    (fd_o_mul<1>): slot j of a lane is column 5h + j, whose bias is 2^25 for
@@ -266,15 +212,6 @@ FD_DEV uint32_t fd_o3_entry( uint32_t q, uint32_t h, int kind, int dw, uint32_t 
     default:         return 0u;
   }
 }
-
-/* this lane's field for op: kind 0/1/2 = bit 7 + bit 5 */
-FD_DEV uint32_t fd_op_kind( uint64_t kw, int op ) {
-  uint32_t k = ((uint32_t)op >> 7) + (((uint32_t)op >> 5) & 1u);
-  return (uint32_t)(kw >> (k << 4));
-}
-/* bit b of a field as a mask (0 / ~0: one v_bfe_i32) or a value */
-FD_DEV uint32_t fd_ok_mask( uint32_t w, int b ) { return (uint32_t)((int32_t)(w << (31 - b)) >> 31); }
-FD_DEV uint32_t fd_ok_bits( uint32_t w, int b, int n ) { return (w >> b) & ((1u << n) - 1u); }
 
 /* A scalar being recoded, as a 256-bit shift register of 8 dwords kept
    normalized: bit 0 of d[0] is the lowest set bit, which sits at scalar

@@ -32,10 +32,6 @@ void h_recode2( uint8_t * ops, int * op_start, uint8_t const * s, uint8_t const 
     op_start[i] = fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, buf, 1 );
   }
 }
-/* the lane-split DSMs' per-lane op decode word (fd_op_kind_word) and a
-   field extracted for an op byte (fd_op_kind) */
-uint64_t h_op_kind_word( uint32_t q ) { return fd_op_kind_word( q ); }
-uint32_t h_op_kind( uint64_t kw, int op ) { return fd_op_kind( kw, op ); }
 void h_fe_mul( int32_t * h, int32_t const * f, int32_t const * g, unsigned long n ) {
   for( unsigned long i=0; i<n; i++ ) {
     fd_gpu_fe_t a, b, c;
@@ -148,7 +144,7 @@ int h_quad_dsm( int32_t * out, int32_t const * A, uint8_t const * ops, int start
   fe bi[8][4];
   for( int e=0; e<8; e++ ) for( int q=0; q<4; q++ ) bi[e][q] = FD_GPU_BI_PRECOMP[e].l[q];
 
-  /* main loop (FD_QUAD_STEP 3: the decode entries of fd_q3_entry, raw
+  /* main loop (the decode entries of fd_q3_entry, raw
      product limbs with their residual masks folded into the entry's
      masks; the same arithmetic the kernel issues, lane by lane) */
   for( int q=0; q<4; q++ ) fd_fe_set( vt[q], q ? 1 : 0 );

@@ -1,4 +1,4 @@
-"""The quad DSM's step (fd_quad_body, FD_QUAD_STEP 3,
+"""The quad DSM's step (fd_quad_body,
 firedancer_amd/csrc/fd_ed25519_gpu_kernels.hip) restated on the host with
 the quad's four lanes as an array (tests/fe_host_harness.cpp h_quad_dsm:
 the same fd_q3_entry decode table, raw products fd_fe_mul_raw and op

@@ -60,38 +60,3 @@ def test_recode_vs_oracle_slide(harness, oracle):  # noqa: F811
             exp, st = expected_stream(oracle, s, k)
             assert start[i] == st, (fn, i, s, k)
             assert (ops[i] == exp).all(), (fn, i, s, k, np.nonzero(ops[i] != exp)[0][:8])
-
-
-def test_op_kind_word(harness):  # noqa: F811
-    """fd_op_kind_word / fd_op_kind (the lane-split DSMs' per-step decode)
-    give, for every lane q and every op byte, the masks the quad and oct
-    kernels computed per step before (their former expressions, restated
-    here from the op byte: add = bit 7, neg = bit 5)."""
-    import ctypes
-    harness.h_op_kind_word.restype = ctypes.c_uint64
-    harness.h_op_kind_word.argtypes = [ctypes.c_uint32]
-    harness.h_op_kind.restype = ctypes.c_uint32
-    harness.h_op_kind.argtypes = [ctypes.c_uint64, ctypes.c_int]
-    M = 0xFFFFFFFF
-    for q in range(4):
-        kw = harness.h_op_kind_word(q)
-        mq = [M if q == j else 0 for j in range(4)]
-        for op in range(256):
-            if op and not (op & 0x80):
-                continue                      # not an op: D is the byte 0, adds have bit 7
-            w = harness.h_op_kind(kw, op)
-            bit = lambda b: M if (w >> b) & 1 else 0  # noqa: E731
-            add = M if op & 0x80 else 0
-            neg = M if (op >> 5) & 1 else 0
-            pos = add & ~neg & M
-            idx = (1 if neg else 2) if q == 0 else 0 if q == 1 else (2 if neg else 1) if q == 2 else 3
-            mW, mT = mq[0] | (mq[2] & add), mq[3] & add
-            gs = 1 if (q == 1 and not add) else 0
-            mP, mQ, qs = mq[0] | (mq[1] & add), mq[3] | (mq[2] & add), 1 if add else 0
-            mR, sR = mq[0] | mq[1] | (~add & M), mq[0] | (mq[3] & ~add & M)
-            mS = ~((mq[0] | mq[1]) & add) & M
-            sS = (mq[0] & ~add & M) | (mq[2] & ~pos & M) | (mq[3] & pos)
-            cadd = (sR & 1) + (sS & 1)
-            got = (bit(0), bit(1), (w >> 2) & 1, bit(3), bit(4), (w >> 5) & 1, bit(6), bit(7), bit(8), bit(9),
-                   (w >> 10) & 3, (w >> 12) & 3)
-            assert got == (mW, mT, gs, mP, mQ, qs, mR, sR, mS, sS, cadd, idx), (q, hex(op))
