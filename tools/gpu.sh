@@ -14,6 +14,7 @@
 #                             4,096-signature quad batch on that library
 #     pmcthr                  PMC passes over the throughput step (VALU, FETCH, WRITE)
 #     pmcsq=lib               the SQ pass alone over the throughput step on a variant library
+#     pmcfetch=lib            the FETCH_SIZE pass alone over the throughput step on a variant library
 #     ringpaced[=args]        tools/ring_paced.py (open-loop 4,096-batch ring)
 #     py=script[,args]        any tools/*.py under a 300 s limit (appends gpurun_out/<script>.out)
 #     libpy=lib:script[,args] the same with FD_ED25519_LIB=lib (a variant library)
@@ -76,6 +77,10 @@ for step in "$@"; do
       pmc thr_p1 "$lib" $P1 -- "${B[@]}" || exit 1
       pmc thr_fetch "$lib" FETCH_SIZE -- "${B[@]}" || exit 1
       pmc thr_write "$lib" WRITE_SIZE -- "${B[@]}" || exit 1 ;;
+    pmcfetch)
+      mkdir -p gpurun_out/pmc
+      tag=$(basename "$arg" .so)
+      pmc "fetch_${tag}" "$R/$arg" FETCH_SIZE -- "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-latency || exit 1 ;;
     pmcsq)
       mkdir -p gpurun_out/pmc
       tag=$(basename "$arg" .so)
