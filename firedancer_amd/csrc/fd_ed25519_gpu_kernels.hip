@@ -143,18 +143,6 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 #ifndef FD_PREP_ZERO
 #define FD_PREP_ZERO 0
 #endif
-/* FD_OPS_SIGMAJOR 1: the throughput path's op streams signature-major as
-   the latency path's ([n][512], each prep lane zeroing its own row; no
-   memset), read by the pooled and uniform DSMs at ops[sg*512 + t].
-   0 (default): step-major [512][n]. */
-#ifndef FD_OPS_SIGMAJOR
-#define FD_OPS_SIGMAJOR 0
-#endif
-#if FD_OPS_SIGMAJOR
-#define FD_OPS_AT(t,sg,n) ((uint64_t)(sg)*FD_OPS_MAX + (uint64_t)(t))
-#else
-#define FD_OPS_AT(t,sg,n) ((uint64_t)(t)*(n) + (uint64_t)(sg))
-#endif
 #define FD_OPS_ZBASE 144
 /* threads per fd_k_prep block (64: each wave's 9 KB stage freed when that
    wave ends rather than when the slowest of four does; no faster, same
@@ -393,7 +381,7 @@ fd_k_prep( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_e
            int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
            uint64_t * __restrict__ kout ) {
   __shared__ __attribute__((aligned(16))) uint8_t sha_stage[(FD_PREP_WG/64)*FD_SHA_STAGE_BYTES];
-  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, kout, FD_OPS_SIGMAJOR );
+  fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, kout, 0 );
 }
 
 /* ------------------------------------------------------------------ */
@@ -783,7 +771,7 @@ fd_k_dsm( uint64_t n, int32_t const * __restrict__ status, int32_t const * __res
   __syncthreads();
   int t0 = fd_wave_min( start );
   for( int t=t0; t<FD_OPS_MAX; t++ ) {
-    int op = (t >= start) ? (int)ops[FD_OPS_AT( t, ii, n )] : 0;
+    int op = (t >= start) ? (int)ops[(uint64_t)t*n + ii] : 0;
     int is_add = op & FD_OP_ADD;
     int neg = (op >> 5) & 1;
     fe E0, E1, E2, E3;
@@ -1937,7 +1925,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       int st = status[sg], pa = pstat[sg], pr = portable ? FD_PT_OK : pstat[n+sg];
       if( st == FD_ST_PENDING && pa == FD_PT_OK && pr == FD_PT_OK ) {
         int t = op_start[sg];
-        mm = (t << 8) | (int)ops[FD_OPS_AT( t, sg, n )];
+        mm = (t << 8) | (int)ops[(uint64_t)t*n + sg];
       }
     }
     mt[j] = mm;
@@ -2042,7 +2030,7 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
       int t = mm >> 8, op = mm & 255;
       uint64_t sg = (uint64_t)gw + (uint64_t)s * nwaves;
       int tn = t + 1;
-      int opn = tn < FD_OPS_MAX ? (int)ops[FD_OPS_AT( tn, sg, n )] : 0;   /* prefetch */
+      int opn = tn < FD_OPS_MAX ? (int)ops[(uint64_t)tn*n + sg] : 0;   /* prefetch */
       /* load, step and store inside each op kind's branch: with the state
          merged after the branch, LLVM gave the new and the old state the
          same registers and copied the old limbs away first (~33 moves per
@@ -2222,7 +2210,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   /* op streams are zeroed by their own prep lanes (only rows of
      signatures still pending after the S check are ever read); the
      FD_PREP_ZERO 0 build memsets the step-major array first */
-  if( !quad && !FD_PREP_ZERO && !FD_OPS_SIGMAJOR ) {
+  if( !quad && !FD_PREP_ZERO ) {
     hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
     if( e != hipSuccess ) return e;
   }
@@ -2315,7 +2303,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * 
                                                    fd_ed25519_gpu_desc_t const * desc, fd_ed25519_gpu_work_t const * w,
                                                    uint64_t * kout, hipStream_t stream ) {
   if( !n ) return hipSuccess;
-  if( !FD_PREP_ZERO && !FD_OPS_SIGMAJOR ) {
+  if( !FD_PREP_ZERO ) {
     hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
     if( e != hipSuccess ) return e;
   }
