@@ -634,6 +634,12 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
         feeder = fa.Feeder(eng)
         starts = np.random.default_rng(seed).permutation(nwin).astype(np.uint64) * BS
         W = window or depth
+        # untimed warm-up: two closed-loop passes over every window, so the
+        # engine's first launches on each slot's CU-group stream and the
+        # first DMA of each page of the freshly registered corpus are not
+        # inside the measured stream (tools/ring_paced_tail.py saw a
+        # ~20 ms stall in a fresh engine's first 60 ms)
+        feeder.synth(base.blob, base.desc, BS, starts, 2 * nwin, depth, 0)
         t0 = time.perf_counter()
         st, codes = feeder.synth(base.blob, base.desc, BS, starts, nb, W, period_ns, codes=True)
         wall = time.perf_counter() - t0
