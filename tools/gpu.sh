@@ -19,6 +19,7 @@
 #     py=script[,args]        any tools/*.py under a 300 s limit (appends gpurun_out/<script>.out)
 #     libpy=lib:script[,args] the same with FD_ED25519_LIB=lib (a variant library)
 #     native=prog[,args]      tools/build/prog (tools/Makefile) under a 300 s limit
+#     env=NAME=VALUE          export NAME=VALUE for the steps after it (A/B knobs)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
@@ -106,6 +107,8 @@ for step in "$@"; do
       timeout -k 10 300 "tools/build/$prog" ${args//,/ } >> "gpurun_out/$prog.jsonl" 2>> "gpurun_out/$prog.err" \
         || { echo "NATIVE $prog FAILED"; tail -20 "gpurun_out/$prog.err"; exit 1; }
       tail -4 "gpurun_out/$prog.jsonl" ;;
+    env)
+      export "$arg"; echo "env $arg" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done

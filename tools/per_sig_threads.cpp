@@ -69,8 +69,11 @@ int main( int argc, char ** argv ) {
     std::sort( L.begin(), L.end() );
     auto pct = [&]( double q ) { return L[ std::min( L.size() - 1, (size_t)( q * (double)L.size() ) ) ] * 1e3; };
     printf( "{\"threads\": %d, \"calls\": %zu, \"calls_per_s\": %.0f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, "
-            "\"rejected\": %d, \"driver\": \"native pthreads\", \"msg\": \"%d-byte random messages\"}\n",
-            T, L.size(), (double)L.size() / dt, pct( 0.5 ), pct( 0.99 ), L.back() * 1e3, bad, MSZ );
+            "\"rejected\": %d, \"driver\": \"native pthreads\", \"msg\": \"%d-byte random messages\", "
+            "\"zc_max\": \"%s\", \"vq_leaders\": \"%s\"}\n",
+            T, L.size(), (double)L.size() / dt, pct( 0.5 ), pct( 0.99 ), L.back() * 1e3, bad, MSZ,
+            getenv( "FD_ED25519_GPU_ZC_MAX" ) ? getenv( "FD_ED25519_GPU_ZC_MAX" ) : "default",
+            getenv( "FD_ED25519_GPU_VQ_LEADERS" ) ? getenv( "FD_ED25519_GPU_VQ_LEADERS" ) : "default" );
     fflush( stdout );
   }
   return 0;
