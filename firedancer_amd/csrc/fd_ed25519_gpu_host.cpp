@@ -109,6 +109,13 @@ extern "C" int fd_ed25519_gpu_wait_selftest( long timeout_ns, long ready_after_n
   return fd_wait_query( fd_fake_query, &f, 1000000L, timeout_ns );
 }
 
+/* direct-output batches of at most this many signatures can be collected
+   by a blocking poll as soon as every code has landed in pinned memory,
+   before the batch's completion event fires (fd_codes_query) */
+#define FD_EARLY_MAX_DEFAULT 64UL
+/* what h_out holds until the DSM writes a code there (no code is this) */
+#define FD_CODE_PENDING ((int32_t)0x7eadc0de)
+
 static inline unsigned long fd_desc_off( unsigned long blob_sz ) { return (blob_sz + FD_BLOB_PAD + 15UL) & ~15UL; }
 
 struct fd_ed25519_gpu_slot {
@@ -130,6 +137,8 @@ struct fd_ed25519_gpu_slot {
   unsigned long           ticket;   /* 0 = free */
   int                     staged;   /* pinned buffers lent out by fd_ed25519_gpu_stage */
   int                     orphan;   /* a synchronous call timed out on it: reclaimed once its event completes */
+  int                     early;    /* codes go straight to h_out over a sentinel: a blocking poll may take them as they land */
+  int                     retiring; /* its codes were taken early: reclaimed once its event completes */
   uint8_t *               h_dig;    /* pinned digests (SHA-512 batch), allocated on first use */
 };
 
@@ -144,6 +153,7 @@ struct fd_ed25519_gpu {
   unsigned long quad_max; /* smaller batches <= this take the quad-lane DSM */
   unsigned long oct_max;  /* and batches <= this the eight-lane DSM */
   unsigned long out_direct_max;  /* ring batches <= this get their codes written to pinned memory by the DSM */
+  unsigned long early_max;       /* and batches <= this may be collected before their completion event (fd_codes_query) */
   unsigned long blob_cap;        /* bytes of a slot's blob buffers (padded blob + descriptors) */
   unsigned long mask_max; /* ring batches <= this run on their slot's CU group */
   int           groups;   /* CU groups the ring's slots are spread over (1: none) */
@@ -286,6 +296,9 @@ extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_new_ex( int device, unsigned long m
        checks the direct path at 40,000 too).  A/B: 0 = always the copy */
     char const * od = getenv( "FD_ED25519_GPU_OUT_DIRECT_MAX" );
     g->out_direct_max = od ? strtoul( od, NULL, 0 ) : 4096UL;
+    /* A/B: 0 = every blocking poll waits for the completion event */
+    char const * em = getenv( "FD_ED25519_GPU_EARLY_MAX" );
+    g->early_max = em ? strtoul( em, NULL, 0 ) : FD_EARLY_MAX_DEFAULT;
   }
   g->device = device; g->max_sigs = max_sigs; g->max_blob = max_blob; g->next_ticket = 1; g->depth = depth;
   __atomic_store_n( &g->timeout_ns, FD_WAIT_TIMEOUT_NS_DEFAULT, __ATOMIC_RELAXED );
@@ -428,9 +441,13 @@ extern "C" void fd_ed25519_gpu_delete( fd_ed25519_gpu_t * g ) {
 
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g->depth : 0; }
 
+static void fd_reclaim_orphans( fd_ed25519_gpu_t * g );
 extern "C" int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * g, int groups ) {
   if( !g || groups < 1 || groups > FD_GPU_DEPTH_MAX ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
+  /* a slot whose codes were taken early is idle for its caller: let it retire */
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].retiring && fd_event_wait( g->slot[s].done, fd_timeout( g ) ) ) return FD_ED25519_ERR_GPU;
+  fd_reclaim_orphans( g );
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket || g->slot[s].staged ) return FD_ED25519_ERR_ARG;   /* ring busy */
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
@@ -562,7 +579,7 @@ extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) {
 static void fd_reclaim_orphans( fd_ed25519_gpu_t * g ) {
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
-    if( sl->orphan && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->ticket = 0; sl->staged = 0; }
+    if( (sl->orphan || sl->retiring) && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->retiring = 0; sl->ticket = 0; sl->staged = 0; }
   }
 }
 
@@ -574,14 +591,32 @@ static void fd_abandon_ticket( fd_ed25519_gpu_t * g, unsigned long ticket ) {
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket == ticket ) g->slot[s].orphan = 1;
 }
 
+/* No slot is free, but one whose codes a poll took early is only retiring
+   (its completion event follows within microseconds): wait for it and
+   reclaim it, so a caller that submits right after such a poll finds the
+   slot as it would have without the early return.  Caller holds g->lock.
+   Returns 1 if a slot came back. */
+static int fd_wait_retiring( fd_ed25519_gpu_t * g ) {
+  for( int s=0; s<g->depth; s++ )
+    if( g->slot[s].retiring ) {
+      if( fd_event_wait( g->slot[s].done, fd_timeout( g ) ) ) return 0;
+      fd_reclaim_orphans( g );
+      return 1;
+    }
+  return 0;
+}
+
 /* Lend a free slot's pinned staging buffers (zero-copy submit). */
 extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
   if( !g || !blob || !desc ) return FD_ED25519_ERR_ARG;
   std::lock_guard<std::mutex> guard( g->lock );
   fd_reclaim_orphans( g );
-  for( int s=0; s<g->depth; s++ ) {
-    fd_ed25519_gpu_slot * sl = &g->slot[s];
-    if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->h_blob; *desc = sl->h_desc; return 0; }
+  for( int pass=0; pass<2; pass++ ) {
+    for( int s=0; s<g->depth; s++ ) {
+      fd_ed25519_gpu_slot * sl = &g->slot[s];
+      if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->h_blob; *desc = sl->h_desc; return 0; }
+    }
+    if( !fd_wait_retiring( g ) ) break;
   }
   return FD_ED25519_ERR_ARG;
 }
@@ -594,7 +629,7 @@ extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob 
 
 /* a free slot: the staged one owning `blob` if any, else any unstaged one
    (slots orphaned by a timed-out synchronous call come back once done) */
-static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * blob ) {
+static fd_ed25519_gpu_slot * fd_free_slot_( fd_ed25519_gpu_t * g, void const * blob ) {
   fd_reclaim_orphans( g );
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && g->slot[s].h_blob == blob ) return &g->slot[s];
   if( g->groups > 1 ) {
@@ -618,6 +653,11 @@ static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * bl
   }
   for( int s=0; s<g->depth; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) return &g->slot[s];
   return NULL;
+}
+static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * blob ) {
+  fd_ed25519_gpu_slot * sl = fd_free_slot_( g, blob );
+  if( !sl && fd_wait_retiring( g ) ) sl = fd_free_slot_( g, blob );
+  return sl;
 }
 extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? g->device : -1; }
 
@@ -824,6 +864,8 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
      ~5 us of every small batch's round trip); they are visible to the
      host once the slot's done event completes */
   int odirect = sl->h_out_dev && n <= g->out_direct_max;
+  sl->early = odirect && n <= g->early_max;
+  if( sl->early ) for( unsigned long i=0; i<n; i++ ) sl->h_out[i] = FD_CODE_PENDING;
   if( (e = fd_ed25519_gpu_launch( n, sl->d_blob, blob_sz, dd, &sl->work, odirect ? sl->h_out_dev : sl->d_out, st,
                                   g->mode, g->pool_min, g->quad_max, g->oct_max )) != hipSuccess )
     return fd_gpu_fail( "launch", e );
@@ -914,6 +956,24 @@ extern "C" int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * g, unsigned long n, voi
   return r == 1 ? 0 : r == 0 ? FD_ED25519_ERR_ARG : r;
 }
 
+/* A small direct-output batch's codes, each written once by the DSM into
+   the slot's coherent pinned h_out over FD_CODE_PENDING: all in means the
+   batch's results are final although the kernel may still be retiring (its
+   completion event, a marker behind it, reaches the host some microseconds
+   later).  Returns 1 all codes in, 2 the event completed, -1 a failed
+   query; the event is queried only every 16th call. */
+struct fd_codes_ctx { fd_ed25519_gpu_slot * sl; unsigned it; };
+static int fd_codes_query( void * p ) {
+  fd_codes_ctx * c = (fd_codes_ctx *)p;
+  volatile int32_t const * o = c->sl->h_out;
+  unsigned long i = 0, n = c->sl->n;
+  while( i < n && o[i] != FD_CODE_PENDING ) i++;
+  if( i == n ) { __atomic_thread_fence( __ATOMIC_ACQUIRE ); return 1; }
+  if( (c->it++ & 15u) ) return 0;
+  int r = fd_event_query( (void *)c->sl->done );
+  return r == 1 ? 2 : r;
+}
+
 extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, int * out, int block ) {
   if( !g || !ticket ) return FD_ED25519_ERR_ARG;
   fd_ed25519_gpu_slot * sl = NULL;
@@ -922,7 +982,22 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
-  if( block ) {
+  if( block && sl->early && out ) {   /* a drain (out NULL) waits for the event */
+    fd_codes_ctx c = { sl, 1u };
+    int r = fd_wait_query( fd_codes_query, &c, FD_POLL_SPIN_NS, fd_timeout( g ) );
+    if( r < 0 ) return FD_ED25519_ERR_GPU;
+    if( r == 0 ) {
+      snprintf( fd_gpu_err, sizeof(fd_gpu_err), "wait: batch not complete after %ld ms", fd_timeout( g ) / 1000000L );
+      return FD_ED25519_ERR_GPU;        /* the ticket stays valid */
+    }
+    if( r == 1 ) {
+      /* the codes are in; the slot comes back once its event completes */
+      std::lock_guard<std::mutex> guard( g->lock );
+      if( out ) fd_slot_collect( sl, out );
+      sl->early = 0; sl->retiring = 1;
+      return 1;
+    }
+  } else if( block ) {
     int err = fd_event_wait( sl->done, fd_timeout( g ) );
     if( err ) return err;               /* timed out or failed; the ticket stays valid */
   } else {
@@ -932,7 +1007,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   }
   std::lock_guard<std::mutex> guard( g->lock );
   if( out ) fd_slot_collect( sl, out );
-  sl->ticket = 0;
+  sl->ticket = 0; sl->early = 0;
   return 1;
 }
 

@@ -195,3 +195,26 @@ print("ok")
         env = dict(os.environ, FD_ED25519_GPU_OUT_DIRECT_MAX=od)
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (od, r.stdout[-1000:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_early_codes_submit_poll_back_to_back(ref, depth):
+    """Round 5: a blocking poll of a direct-output batch of at most
+    early_max (64) signatures returns as soon as every code has landed in
+    the slot's pinned memory, before the completion event; the slot then
+    retires.  Back-to-back submit -> poll on a one-slot engine must still
+    find its slot (fd_wait_retiring), and every code must equal the
+    reference's -- batches of 1, 17, 64 (early) and 65 (event) on the oct
+    and quad DSMs, with invalid signatures mixed in."""
+    b = corpus.adversarial(128, 200, seed=51, invalid_frac=0.4)
+    exp = oracle_batch(ref, b)
+    e = fa.Engine(0, 128, 1 << 20, depth=depth)
+    for rep in range(40):
+        for n in (1, 17, 64, 65):
+            lo = (rep * 7) % (128 - n + 1)
+            sub = corpus.Batch(b.blob, b.desc[lo:lo + n])
+            t = e.submit(sub.blob, sub.desc)
+            got = np.full(n, 99, np.int32)
+            assert e.poll(t, got, True)
+            assert (got == exp[lo:lo + n]).all(), (rep, n, lo, int((got != exp[lo:lo + n]).sum()))
+    e.close()
