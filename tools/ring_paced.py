@@ -35,6 +35,7 @@ def main():
         r = bench.ring_stream(fa, ring, 0, nb, depth, window=2 * depth, period_ns=int(round(bench.BATCH_SIGS / (mps * 1e6) * 1e9)), expected=exp)
         out[f"paced_{mps:g}"] = {"mps": r["pcie_inclusive_verifies_per_s"] / 1e6, "sched_p50_ms": r["sched_to_done_p50_ms"],
                                  "sched_p99_ms": r["sched_to_done_p99_ms"], "sched_max_ms": r["sched_to_done_max_ms"],
+                                 "push_submit_p99_ms": r["push_to_submit_p99_ms"], "submit_done_p99_ms": r["submit_to_done_p99_ms"],
                                  "mismatches": r["mismatches"]}
     print(json.dumps(out), flush=True)
 
