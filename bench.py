@@ -586,7 +586,9 @@ def latency_legs(fa, corpus, a, device):
         # up to 2 x depth outstanding: the feeder always holds the next batch
         # when a slot frees; what the ring cannot take waits in its queue
         # and that wait is part of sched -> done
-        r = ring_stream(fa, ring, device, nb2, a.ring_depth, window=2 * a.ring_depth,
+        # each offered load over the full >= 10^4 batches (C2's
+        # p50 / p99 over at least 10^4 batches; round 4 ran half of that)
+        r = ring_stream(fa, ring, device, nb, a.ring_depth, window=2 * a.ring_depth,
                         period_ns=int(round(BATCH_SIGS / (mps * 1e6) * 1e9)), expected=exp)
         paced.append(r)
     lat["paced"] = paced
