@@ -117,15 +117,17 @@ FD_EXPORT int fd_vt_tcache_insert( fd_vt_tcache_t * tc, unsigned long tag ) {
 /* ---- the tile ------------------------------------------------------------ */
 
 struct fd_vt_txn {
-  uint64_t blob_off, sz, ctl, tsorig, tag;
+  uint64_t blob_off, sz, ctl, tsorig, tag, seq;   /* seq: input mcache seq, FD_VT_NOSEQ if none */
   uint32_t sig0, nsig;
 };
+#define FD_VT_NOSEQ (~0UL)
 
 struct fd_vt_batch {
   uint8_t *               blob;   /* engine slot's pinned staging buffers (feeder mode: this batch's host buffers) */
   fd_ed25519_gpu_desc_t * desc;
   unsigned long           used, nsig, ticket;
   unsigned long           first;  /* receive index of the batch's first frag */
+  unsigned long           t_open; /* CLOCK_MONOTONIC ns at the batch's first frag (the wait bound) */
   /* in-place mode: a batch that continues past the wrap of the caller's
      frag ring is two spans, [blob, blob+alen) then blob2 onwards (alen 0:
      one span); offsets (desc, txn blob_off, used) index their
@@ -170,6 +172,12 @@ struct fd_verify_tile {
   uint8_t const *           ip_region;
   unsigned long             ip_region_sz;
   unsigned long             rx_cnt;       /* frags received (rx calls) */
+  long                      max_wait;     /* open-batch wait bound, ns (< 0: size only) */
+  /* overrun checks (fd_verify_tile_set_ovrn) */
+  fd_verify_tile_ovrn_fn    ovrn;
+  fd_verify_tile_chunk_fn   chunk;
+  void *                    octx;
+  std::vector<uint8_t>      bounce;       /* in place, no chunk callback: the publish copy */
 };
 
 /* A frag into the open batch with streaming (non-temporal) stores: the
@@ -225,14 +233,29 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
   }
   unsigned long tspub = fd_vt_now();
   FD_VT_STAMP( p0 );
+  /* in place with overrun checks: the frag's bytes are still the
+     producer's; copy them out, then re-check the seq (the reference
+     consumer's "overrun while processing" check,
+     test_wiredancer_demo.c:437-441) -- a frag whose seq is still current
+     was unchanged from rx through the device's DMA and the copy */
+  int const ocheck = t->ovrn && t->inplace;
   for( fd_vt_txn const & x : b->txns ) {
     int ok = 1;
     for( uint32_t k=0; k<x.nsig; k++ ) ok &= ( codes[ x.sig0 + k ] == FD_ED25519_SUCCESS );
-    if( ok ) {
-      if( t->publish ) {
-        uint8_t const * fp = ( b->alen && x.blob_off >= b->alen ) ? b->blob2 + (x.blob_off - b->alen) : b->blob + x.blob_off;
-        t->publish( t->ctx, x.tag, fp, x.sz, x.ctl, x.tsorig, tspub );
+    uint8_t const * fp = NULL;
+    if( ok && ( t->publish || ocheck ) )
+      fp = ( b->alen && x.blob_off >= b->alen ) ? b->blob2 + (x.blob_off - b->alen) : b->blob + x.blob_off;
+    if( ocheck && x.seq != FD_VT_NOSEQ ) {
+      if( ok && t->publish ) {
+        uint8_t * dst = t->chunk ? (uint8_t *)t->chunk( t->octx, x.sz ) : NULL;
+        if( !dst ) { if( t->bounce.size() < x.sz ) t->bounce.resize( x.sz ); dst = t->bounce.data(); }
+        memcpy( dst, fp, x.sz );
+        fp = dst;
       }
+      if( t->ovrn( t->octx, x.seq ) ) { t->diag[ FD_VERIFY_TILE_DIAG_OVRN_CNT ]++; continue; }
+    }
+    if( ok ) {
+      if( t->publish ) t->publish( t->ctx, x.tag, fp, x.sz, x.ctl, x.tsorig, tspub );
       t->diag[ FD_VERIFY_TILE_DIAG_PUB_CNT ]++;
       t->diag[ FD_VERIFY_TILE_DIAG_PUB_SZ  ] += x.sz;
     } else {
@@ -353,15 +376,23 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
 static int fd_vt_reserve_inplace( fd_verify_tile_t * t, uint8_t const * f, unsigned long nsig, unsigned long sz ) {
   fd_vt_batch * b = t->open;
   if( b ) {
+    /* a span may reach at most half the region: a producer that honours
+       fd_verify_tile_held can always write the other half while the batch
+       is verified (with a whole-region span it could never write the frag
+       that would close the batch) */
+    unsigned long const half = t->ip_region_sz / 2UL;
     int close = b->nsig + nsig > t->batch_sigs;
     if( !close && !b->alen ) {
-      if( f >= b->blob ) close = (unsigned long)(f - b->blob) + sz > t->max_blob;
-      else {                                    /* the ring wrapped: a second span from f */
-        close = b->used + sz > t->max_blob || f + sz > b->blob;
+      if( f >= b->blob ) {
+        unsigned long ext = (unsigned long)(f - b->blob) + sz;
+        close = ext > t->max_blob || ext > half;
+      } else {                                  /* the ring wrapped: a second span from f */
+        close = b->used + sz > t->max_blob || f + sz > b->blob || b->used + sz > half;
         if( !close ) { b->alen = b->used; b->blob2 = f; }
       }
     } else if( !close ) {
-      close = f < b->blob2 || f + sz > b->blob || b->alen + (unsigned long)(f - b->blob2) + sz > t->max_blob;
+      unsigned long ext = f < b->blob2 ? 0UL : b->alen + (unsigned long)(f - b->blob2) + sz;
+      close = f < b->blob2 || f + sz > b->blob || ext > t->max_blob || ext > half;
     }
     if( close ) {
       int err = fd_vt_submit( t );
@@ -421,7 +452,7 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
 FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
                                                  fd_verify_tile_publish_fn publish, void * ctx ) {
   if( !gpu ) return NULL;
-  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL };
+  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL, 0L };
   if( cfg ) c = *cfg;
   unsigned long maxs = fd_ed25519_gpu_max_sigs( gpu );
   if( !c.batch_sigs || c.batch_sigs > maxs ) c.batch_sigs = maxs;
@@ -431,6 +462,7 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
   fd_verify_tile_t * t = new fd_verify_tile_t();
   t->gpu = gpu; t->publish = publish; t->ctx = ctx; t->tc = tc;
   t->batch_sigs = c.batch_sigs;
+  t->max_wait = c.max_wait_ns ? c.max_wait_ns : FD_VERIFY_TILE_MAX_WAIT_DEFAULT;
   t->max_blob = fd_ed25519_gpu_max_blob( gpu );
   t->open = NULL;
   int depth = fd_ed25519_gpu_depth( gpu );
@@ -453,7 +485,7 @@ static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsi
                                            void const * ip_region, unsigned long ip_region_sz ) {
   if( !gpus || !gpu_cnt || gpu_cnt > FD_VERIFY_TILE_GPU_MAX ) return NULL;
   for( unsigned long e=0; e<gpu_cnt; e++ ) if( !gpus[e] ) return NULL;
-  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL };
+  fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL, 0L };
   if( cfg ) c = *cfg;
   unsigned long maxs = ~0UL, maxb = ~0UL;
   for( unsigned long e=0; e<gpu_cnt; e++ ) {
@@ -468,6 +500,7 @@ static fd_verify_tile_t * fd_vt_new_multi( fd_ed25519_gpu_t * const * gpus, unsi
   fd_verify_tile_t * t = new fd_verify_tile_t();
   t->gpu = gpus[0]; t->publish = publish; t->ctx = ctx; t->tc = tc;
   t->batch_sigs = c.batch_sigs; t->max_blob = maxb; t->open = NULL;
+  t->max_wait = c.max_wait_ns ? c.max_wait_ns : FD_VERIFY_TILE_MAX_WAIT_DEFAULT;
   t->multi = 1; t->gpu_cnt = (int)gpu_cnt; t->next = 0;
   t->inplace = ip_region != NULL; t->ip_region = (uint8_t const *)ip_region; t->ip_region_sz = ip_region_sz;
   memset( t->diag, 0, sizeof(t->diag) );
@@ -579,9 +612,15 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
        timeout, then report the registration as leaked rather than drop it
        silently (it would keep its refcount and make a later
        register of the same pointer with another size fail) */
+    /* one deadline for the whole retry (each unregister may itself wait up
+       to the engine timeout on a slot's event); only a device-side failure
+       (ERR_GPU: a slot still reads the region) is worth retrying -- any
+       other result (ERR_ARG: the registration is gone) ends it, and with
+       no engine timeout (< 0) it is tried once */
     int r = fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
     long to = fd_ed25519_gpu_timeout( t->gpu );
-    for( long w = 0; r && (to < 0 || w < to); w += 1000000L ) {
+    unsigned long t0 = fd_vt_now();
+    while( r == FD_ED25519_ERR_GPU && to >= 0 && fd_vt_now() - t0 < (unsigned long)to ) {
       struct timespec ts = { 0, 1000000L }; nanosleep( &ts, NULL );
       r = fd_ed25519_gpu_unregister( t->gpu, (void *)t->ip_region );
     }
@@ -620,13 +659,25 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
 }
 
 static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
-                                unsigned long tsorig );
+                                unsigned long tsorig, unsigned long seq );
 
 FD_EXPORT int fd_verify_tile_rx( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
                                  unsigned long tsorig ) {
-  int err = fd_verify_tile_rx_( t, frag, sz, ctl, tsorig );
+  int err = fd_verify_tile_rx_( t, frag, sz, ctl, tsorig, FD_VT_NOSEQ );
   t->rx_cnt++;
   return err;
+}
+
+FD_EXPORT int fd_verify_tile_rx_seq( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
+                                     unsigned long tsorig, unsigned long seq ) {
+  int err = fd_verify_tile_rx_( t, frag, sz, ctl, tsorig, seq == FD_VT_NOSEQ ? FD_VT_NOSEQ - 1UL : seq );
+  t->rx_cnt++;
+  return err;
+}
+
+FD_EXPORT void fd_verify_tile_set_ovrn( fd_verify_tile_t * t, fd_verify_tile_ovrn_fn ovrn, fd_verify_tile_chunk_fn chunk,
+                                        void * ctx ) {
+  t->ovrn = ovrn; t->chunk = chunk; t->octx = ctx;
 }
 
 FD_EXPORT unsigned long fd_verify_tile_held( fd_verify_tile_t const * t ) {
@@ -637,8 +688,13 @@ FD_EXPORT unsigned long fd_verify_tile_held( fd_verify_tile_t const * t ) {
 }
 
 static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned long sz, unsigned long ctl,
-                                unsigned long tsorig ) {
+                                unsigned long tsorig, unsigned long seq ) {
   uint8_t const * f = (uint8_t const *)frag;
+  /* overrun checks (fd_verify_tile_set_ovrn): in place right after the
+     speculative trailer / tag reads (as the reference's dedup checks the
+     seq before its tcache insert, fd_dedup.c:512-522); copying, after the
+     frag's copy into the batch and before it is committed to it */
+  int const oc = t->ovrn && seq != FD_VT_NOSEQ;
 #ifdef FD_VT_PROF
   fd_vt_prof[6]++;
 #endif
@@ -660,13 +716,16 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
     unsigned long tag;
     memcpy( &tag, f + hdr.signature_off, 8 );
     FD_VT_STAMP( s1 ); FD_VT_ACC( 0, s0, s1 );
-    int dup = fd_vt_tcache_insert( t->tc, tag );
-    FD_VT_STAMP( s2 ); FD_VT_ACC( 1, s1, s2 );
-    if( dup ) {
-      t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;
-      t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_SZ  ] += sz;
-      return 0;
+    if( !oc || t->inplace ) {
+      if( oc && t->ovrn( t->octx, seq ) ) { t->diag[ FD_VERIFY_TILE_DIAG_OVRN_CNT ]++; return 0; }
+      int dup = fd_vt_tcache_insert( t->tc, tag );
+      if( dup ) {
+        t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;
+        t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_SZ  ] += sz;
+        return 0;
+      }
     }
+    FD_VT_STAMP( s2 ); FD_VT_ACC( 1, s1, s2 );
     unsigned long room, base;
     fd_vt_batch * b;
     if( t->inplace ) {
@@ -688,6 +747,17 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
       base = b->used;
       fd_vt_copy_nt( b->blob + base, f, sz );
       FD_VT_STAMP( s4 ); FD_VT_ACC( 3, s3, s4 );
+      if( oc ) {
+        /* the copy is not committed yet (b->used unchanged): an overrun
+           frag or a duplicate leaves the batch as it was */
+        _mm_sfence();
+        if( t->ovrn( t->octx, seq ) ) { t->diag[ FD_VERIFY_TILE_DIAG_OVRN_CNT ]++; return 0; }
+        if( fd_vt_tcache_insert( t->tc, tag ) ) {
+          t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;
+          t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_SZ  ] += sz;
+          return 0;
+        }
+      }
     }
     FD_VT_STAMP( s4 );
     for( unsigned long k=0; k<nsig; k++ ) {
@@ -697,8 +767,8 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
       d->msg_off = (uint32_t)(base + hdr.message_off);
       d->msg_sz  = (uint32_t)(psz - hdr.message_off);
     }
-    fd_vt_txn x = { base, sz, ctl, tsorig, tag, (uint32_t)b->nsig, (uint32_t)nsig };
-    if( b->txns.empty() ) b->first = t->rx_cnt;
+    fd_vt_txn x = { base, sz, ctl, tsorig, tag, seq, (uint32_t)b->nsig, (uint32_t)nsig };
+    if( b->txns.empty() ) { b->first = t->rx_cnt; b->t_open = fd_vt_now(); }
     b->txns.push_back( x );
     b->nsig += nsig;
     b->used += room;
@@ -708,7 +778,9 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
     return 0;
   }
 bad:
-  t->diag[ FD_VERIFY_TILE_DIAG_BAD_CNT ]++;
+  /* a frag that does not parse may be one its producer is overwriting */
+  if( oc && t->ovrn( t->octx, seq ) ) t->diag[ FD_VERIFY_TILE_DIAG_OVRN_CNT ]++;
+  else                                 t->diag[ FD_VERIFY_TILE_DIAG_BAD_CNT ]++;
   return 0;
 }
 
@@ -766,7 +838,20 @@ FD_EXPORT int fd_verify_tile_service( fd_verify_tile_t * t, int flush ) {
     while( !t->inflight.empty() ) if( (err = fd_vt_drain( t, 1 )) ) return err;
     return 0;
   }
-  return fd_vt_drain( t, 0 );
+  int err = fd_vt_drain( t, 0 );
+  if( err ) return err;
+  /* the wait bound: a partly filled batch goes to the device once its
+     oldest frag has waited max_wait, or at once when nothing is in flight
+     (the device is idle: waiting for more frags only adds latency).  Under
+     load batches still close full (rx), and while they are in flight the
+     open batch keeps filling: its size follows the offered load. */
+  fd_vt_batch * b = t->open;
+  if( b && b->nsig && t->max_wait >= 0
+      && ( t->inflight.empty() || fd_vt_now() - b->t_open >= (unsigned long)t->max_wait ) ) {
+    t->diag[ FD_VERIFY_TILE_DIAG_AGE_CNT ]++;
+    if( (err = fd_vt_submit( t )) ) return err;
+  }
+  return 0;
 }
 
 FD_EXPORT void fd_verify_tile_diag( fd_verify_tile_t const * t, unsigned long * diag ) {

@@ -98,7 +98,9 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
   if( !a->gpu || !a->tile ) {
     a->err = FD_ED25519_ERR_GPU;
     if( a->cnc ) fd_vt_cnc_set( a->cnc, FD_VERIFY_TILE_SIGNAL_FAIL );
+    return;
   }
+  if( a->ovrn ) fd_verify_tile_set_ovrn( a->tile, a->ovrn, a->chunk, a->ovrn_ctx );
 }
 
 static void fd_vt_diag_push( fd_verify_tile_args_t * a, int in_backp, unsigned long backp_cnt ) {
@@ -111,7 +113,7 @@ static void fd_vt_diag_push( fd_verify_tile_args_t * a, int in_backp, unsigned l
 
 static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
   fd_verify_tile_cnc_t * cnc = a->cnc;
-  if( a->err || !cnc || !a->in ) { a->err = a->err ? a->err : FD_ED25519_ERR_ARG; if( cnc ) fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
+  if( a->err || !cnc || !( a->in || a->in_seq ) ) { a->err = a->err ? a->err : FD_ED25519_ERR_ARG; if( cnc ) fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
   if( fd_vt_cnc_query( cnc ) != FD_VERIFY_TILE_SIGNAL_BOOT ) { a->err = FD_ED25519_ERR_ARG; fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
   int           in_backp  = 1;          /* as the reference tile boots (fd_frank_verify.c:46-52) */
   unsigned long backp_cnt = 0UL;
@@ -125,7 +127,7 @@ static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
     if( now - then >= 0L ) {
       /* housekeeping (fd_frank_verify.c:143-182) */
       __atomic_store_n( &cnc->heartbeat, now, __ATOMIC_RELAXED );
-      int err = fd_verify_tile_service( a->tile, 0 );      /* publish completed batches, in order */
+      int err = fd_verify_tile_service( a->tile, 0 );      /* publish completed batches, in order; the wait bound */
       if( err ) { a->err = err; fd_vt_diag_push( a, in_backp, backp_cnt ); fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
       fd_vt_diag_push( a, in_backp, backp_cnt );
       unsigned long s = fd_vt_cnc_query( cnc );
@@ -147,12 +149,21 @@ static void fd_vt_task_run( fd_verify_tile_args_t * a ) {
       continue;
     }
     /* the frag path (the reference's placeholder, :196-203) */
-    void const * frag; unsigned long sz, ctl, tsorig;
-    if( a->in( a->in_ctx, &frag, &sz, &ctl, &tsorig ) > 0 ) {
-      int err = fd_verify_tile_rx( a->tile, frag, sz, ctl, tsorig );
+    void const * frag; unsigned long sz, ctl, tsorig, seq;
+    int got = a->in_seq ? a->in_seq( a->in_ctx, &frag, &sz, &ctl, &tsorig, &seq )
+                        : a->in    ( a->in_ctx, &frag, &sz, &ctl, &tsorig );
+    if( got > 0 ) {
+      int err = a->in_seq ? fd_verify_tile_rx_seq( a->tile, frag, sz, ctl, tsorig, seq )
+                          : fd_verify_tile_rx    ( a->tile, frag, sz, ctl, tsorig );
       if( err ) { a->err = err; fd_vt_diag_push( a, in_backp, backp_cnt ); fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
       if( cr_avail != ~0UL ) cr_avail--;
     } else {
+      /* input idle: publish what landed and apply the wait bound now
+         rather than at the next housekeeping (a lone frag at an idle tile
+         goes to the device at once, as the reference verifies each frag
+         as it arrives, fd_frank_verify_synth_load.c:378-410) */
+      int err = fd_verify_tile_service( a->tile, 0 );
+      if( err ) { a->err = err; fd_vt_diag_push( a, in_backp, backp_cnt ); fd_vt_cnc_set( cnc, FD_VERIFY_TILE_SIGNAL_FAIL ); return; }
       __builtin_ia32_pause();
     }
     now = fd_vt_now();

@@ -9,14 +9,15 @@ import numpy as np
 from . import EngineError, _p, last_error, lib
 
 DIAG = ("IN_BACKP", "BACKP_CNT", "HA_FILT_CNT", "HA_FILT_SZ", "SV_FILT_CNT", "SV_FILT_SZ",
-        "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT", "RING_FULL_CNT")
+        "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT", "RING_FULL_CNT", "OVRN_CNT", "AGE_CNT")
 
 PUBLISH_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_ulong,
                               ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong)
 
 
 class Cfg(ctypes.Structure):
-    _fields_ = [("batch_sigs", ctypes.c_ulong), ("tcache_depth", ctypes.c_ulong), ("tcache_map_cnt", ctypes.c_ulong)]
+    _fields_ = [("batch_sigs", ctypes.c_ulong), ("tcache_depth", ctypes.c_ulong), ("tcache_map_cnt", ctypes.c_ulong),
+                ("max_wait_ns", ctypes.c_long)]
 
 
 class TCache:
@@ -87,7 +88,8 @@ class VerifyTile:
     lat=LatHist() records tsorig -> tspub natively instead; otherwise
     publishes are only counted."""
 
-    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True, lat=None, region=None):
+    def __init__(self, engine, batch_sigs=0, tcache_depth=16, tcache_map_cnt=64, collect=True, lat=None, region=None,
+                 max_wait_ns=0):
         """region (a contiguous uint8 array): the in-place mode
         (fd_verify_tile_new_inplace) -- every frag handed to rx_burst* lies
         in it and is DMA'd from where it lies, no copy; it must stay
@@ -96,7 +98,7 @@ class VerifyTile:
         self._region = region
         self.published = []
         self._cb = PUBLISH_FN(self._on_publish) if collect and lat is None else None
-        cfg = Cfg(batch_sigs, tcache_depth, tcache_map_cnt)
+        cfg = Cfg(batch_sigs, tcache_depth, tcache_map_cnt, max_wait_ns)
         cb = ctypes.cast(self._cb, ctypes.c_void_p) if self._cb else None
         ctx = None
         if lat is not None:                       # native latency histogram (LatHist)
@@ -196,7 +198,9 @@ class Args(ctypes.Structure):
                 ("allow_syscalls", ctypes.POINTER(ctypes.c_long)),
                 ("gpu", ctypes.c_void_p), ("tile", ctypes.c_void_p), ("err", ctypes.c_int),
                 ("device_cnt", ctypes.c_int), ("gpus", ctypes.c_void_p * GPU_MAX),
-                ("region", ctypes.c_void_p), ("region_sz", ctypes.c_ulong)]
+                ("region", ctypes.c_void_p), ("region_sz", ctypes.c_ulong),
+                ("in_seq", ctypes.c_void_p), ("ovrn", ctypes.c_void_p), ("chunk", ctypes.c_void_p),
+                ("ovrn_ctx", ctypes.c_void_p)]
 
 
 class TaskFns(ctypes.Structure):
@@ -210,7 +214,7 @@ class Task:
     another thread) or the task fails."""
 
     def __init__(self, frags, device=0, max_sigs=4096, max_blob=8 << 20, depth=3, batch_sigs=0,
-                 credits=None, lazy_ns=0, device_cnt=0):
+                 credits=None, lazy_ns=0, device_cnt=0, max_wait_ns=0):
         L = lib()
         L.fd_verify_tile_task_get.restype = ctypes.POINTER(TaskFns)
         fns = L.fd_verify_tile_task_get().contents
@@ -229,7 +233,7 @@ class Task:
         self._cr = CR_FN(self._on_cr) if credits is not None else None
         a = Args()
         a.device, a.max_sigs, a.max_blob, a.depth = device, max_sigs, max_blob, depth
-        a.cfg = Cfg(batch_sigs, 16, 64)
+        a.cfg = Cfg(batch_sigs, 16, 64, max_wait_ns)
         a.cnc = ctypes.pointer(self.cnc)
         a.in_fn = ctypes.cast(self._in, ctypes.c_void_p)
         a.publish = ctypes.cast(self._pub, ctypes.c_void_p)

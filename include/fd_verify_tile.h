@@ -56,7 +56,9 @@ extern "C" {
 #define FD_VERIFY_TILE_DIAG_SIG_CNT     (9UL)  /* signatures sent to the GPU */
 #define FD_VERIFY_TILE_DIAG_BATCH_CNT   (10UL) /* GPU batches submitted      */
 #define FD_VERIFY_TILE_DIAG_RING_FULL_CNT (11UL) /* waits for a free ring slot */
-#define FD_VERIFY_TILE_DIAG_CNT         (12UL)
+#define FD_VERIFY_TILE_DIAG_OVRN_CNT    (12UL) /* frags dropped: overrun by their producer (fd_verify_tile_set_ovrn) */
+#define FD_VERIFY_TILE_DIAG_AGE_CNT     (13UL) /* batches closed below size by the wait bound (max_wait_ns) */
+#define FD_VERIFY_TILE_DIAG_CNT         (14UL)
 /* IN_BACKP / BACKP_CNT are the flow-control backpressure diagnostics of
    the reference (fd_frank_verify.c:185-194): maintained by the task's run
    loop (fd_verify_tile_task below); the bare tile object reports 0. */
@@ -65,7 +67,16 @@ typedef struct {
   unsigned long batch_sigs;      /* signatures per GPU batch (<= engine max_sigs); 0 -> engine max */
   unsigned long tcache_depth;    /* HA dedup window; reference uses 16 (fd_frank_verify.c:112) */
   unsigned long tcache_map_cnt;  /* power of 2 >= depth+2; reference uses 64 */
+  long          max_wait_ns;     /* bound on a frag's wait in the open batch (see fd_verify_tile_service):
+                                    0 -> FD_VERIFY_TILE_MAX_WAIT_DEFAULT, < 0 -> batches close on size only */
 } fd_verify_tile_cfg_t;
+
+/* The reference tile verifies and publishes each frag as it arrives
+   (fd_frank_verify_synth_load.c:378-410); a batching tile must not hold a
+   partly filled batch indefinitely under light load.  Default bound: the
+   open batch is submitted once its oldest frag has waited 100 us, or at
+   once when nothing is in flight. */
+#define FD_VERIFY_TILE_MAX_WAIT_DEFAULT (100000L)
 
 /* publish callback: the fd_mcache_publish arguments
    (fd_frank_verify_synth_load.c:405-410) with the frag bytes in place of
@@ -90,9 +101,10 @@ fd_verify_tile_new( fd_ed25519_gpu_t *           gpu,
 /* Multi-engine (feeder) mode: one tile driving gpu_cnt engines (at most
    FD_VERIFY_TILE_GPU_MAX, e.g. one per GPU of the node), each through its
    per-GPU feeder thread (fd_ed25519_gpu_feeder_*, NUMA-pinned, whole ring
-   in flight).  Batches are built in host buffers owned per engine (2 x its
-   ring depth, registered with it so the feeder DMAs them in place) and go
-   to the engines round robin; publishes stay in arrival order.  Same
+   in flight).  Batches are built in host buffers shared by the engines
+   (registered with each, so any engine's feeder DMAs them in place) and a
+   closed batch goes to the engine with the fewest signatures still on its
+   device (ties round robin); publishes stay in arrival order.  Same
    semantics and counters as fd_verify_tile_new; RING_FULL_CNT counts waits
    for a free batch buffer.  The engines must outlive the tile.  Lets the
    reference's verify_tile_count (src/app/fdctl/config/default.toml:297-299)
@@ -111,12 +123,13 @@ fd_verify_tile_new_multi( fd_ed25519_gpu_t * const *   gpus,
    from directly: the frag path copies nothing.  A batch is the span of
    its frags; frags arrive at increasing addresses, and at the caller's
    ring wrap the open batch continues as a second span from the lower
-   address (two DMA pieces, fd_ed25519_gpu_try_submit2); a second wrap
-   closes it.  A frag's bytes must stay
-   unchanged until it is published or dropped (the reference's flow
-   control: credits return after the frag is consumed).  NULL if the
-   region cannot be registered.  Same semantics and counters as
-   fd_verify_tile_new otherwise. */
+   address (two DMA pieces, fd_ed25519_gpu_try_submit2); a second wrap,
+   or a span reaching half the region, closes it.  A frag's bytes must
+   either stay unchanged until it is published or dropped (a producer
+   that honours fd_verify_tile_held), or be checked for overrun
+   (fd_verify_tile_set_ovrn: the reference's QUIC -> verify link, which
+   has no credits).  NULL if the region cannot be registered.  Same
+   semantics and counters as fd_verify_tile_new otherwise. */
 fd_verify_tile_t *
 fd_verify_tile_new_inplace( fd_ed25519_gpu_t *           gpu,
                             fd_verify_tile_cfg_t const * cfg,
@@ -184,9 +197,57 @@ typedef struct {
 void fd_verify_tile_lat_publish( void * ctx, unsigned long sig, void const * frag, unsigned long sz,
                                  unsigned long ctl, unsigned long tsorig, unsigned long tspub );
 
-/* Housekeeping: publish every completed batch without blocking; if
-   flush, also submit the partial batch and wait for all in flight. */
+/* Housekeeping: publish every completed batch without blocking, then
+   close the open (partly filled) batch if its oldest frag has waited
+   max_wait_ns or the engine has nothing in flight (max_wait_ns >= 0; a
+   full batch closes on size in rx), so every frag reaches a batch within
+   max_wait_ns of the call that follows its receipt; if flush, submit the
+   partial batch regardless and wait for all in flight.  The task's run
+   loop calls it at every housekeeping and on every idle input poll. */
 int fd_verify_tile_service( fd_verify_tile_t * tile, int flush );
+
+/* ---- Overrun safety (the reference's QUIC -> verify link) -------------
+
+   The reference's link into the verify tile has no credit flow control:
+   a slow consumer is overrun and frags "begin being dropped"
+   (src/app/fdctl/config/default.toml:473-477).  Its consumers read a frag
+   speculatively and then re-check the frag's mcache seq: a lapped seq
+   means the bytes may have been overwritten, and the frag is dropped
+   (src/disco/dedup/fd_dedup.c:512-522; src/wiredancer/test/
+   test_wiredancer_demo.c:437-441).  With an ovrn callback set, frags
+   received with their seq (fd_verify_tile_rx_seq) get the same check:
+     copy modes: after the frag's copy into the batch (before it is
+       committed to it), so a batch holds only bytes read while the frag
+       was intact;
+     in-place modes: at rx (after the trailer and tag reads) and again at
+       publish, after the tile copied the frag's bytes to the publish chunk
+       (chunk(ctx, sz), or a tile-owned buffer if chunk is NULL) -- the
+       device DMA'd the frag between the two, so a frag whose seq is still
+       current at the second check was unchanged from rx through the copy:
+       the bytes published are the bytes verified.
+   A failed check drops the frag and counts OVRN_CNT (before the tcache
+   insert at rx; instead of SV_FILT at publish).  ovrn(ctx, seq) returns
+   nonzero iff seq has been overrun (its mcache line no longer holds seq);
+   it must order the caller's earlier reads of the frag before its own
+   read of the line (an acquire fence).  The producer's dcache must hold
+   at least depth + 1 frags of maximum size (fd_dcache_req_data_sz's burst
+   slack), so a frag's bytes are rewritten only after its line is lapped. */
+typedef int    (*fd_verify_tile_ovrn_fn )( void * ctx, unsigned long seq );
+typedef void * (*fd_verify_tile_chunk_fn)( void * ctx, unsigned long sz );
+void fd_verify_tile_set_ovrn( fd_verify_tile_t *      tile,
+                              fd_verify_tile_ovrn_fn  ovrn,
+                              fd_verify_tile_chunk_fn chunk,
+                              void *                  ctx );
+
+/* fd_verify_tile_rx of a frag with its input mcache seq (overrun checks
+   above; rx and rx_burst frags are never checked). */
+int
+fd_verify_tile_rx_seq( fd_verify_tile_t * tile,
+                       void const *       frag,
+                       unsigned long      sz,
+                       unsigned long      ctl,
+                       unsigned long      tsorig,
+                       unsigned long      seq );
 
 /* Frags received so far below which the tile reads no frag any more:
    the receive index (0-based count of rx calls) of the oldest frag an
@@ -231,6 +292,9 @@ typedef struct {
    reference tile's mcache poll) */
 typedef int (*fd_verify_tile_in_fn)( void * ctx, void const ** frag, unsigned long * sz,
                                      unsigned long * ctl, unsigned long * tsorig );
+/* the same with the frag's input mcache seq (*seq), for overrun checks */
+typedef int (*fd_verify_tile_in_seq_fn)( void * ctx, void const ** frag, unsigned long * sz,
+                                         unsigned long * ctl, unsigned long * tsorig, unsigned long * seq );
 /* downstream credits available (fd_fctl_tx_cr_update); 0 = backpressured */
 typedef unsigned long (*fd_verify_tile_cr_fn)( void * ctx );
 
@@ -267,6 +331,14 @@ typedef struct {
      fd_verify_tile_held( args->tile ) */
   void const *               region;
   unsigned long              region_sz;
+  /* overrun safety (set by the caller, optional): in_seq replaces in and
+     hands each frag's mcache seq to the tile; ovrn / chunk / ovrn_ctx as
+     fd_verify_tile_set_ovrn (the reference's credit-less QUIC -> verify
+     link) */
+  fd_verify_tile_in_seq_fn   in_seq;
+  fd_verify_tile_ovrn_fn     ovrn;
+  fd_verify_tile_chunk_fn    chunk;
+  void *                     ovrn_ctx;
 } fd_verify_tile_args_t;
 
 typedef struct {

@@ -33,7 +33,7 @@ extern "C" int LLVMFuzzerTestOneInput( uint8_t const * data, size_t size ) {
     r = tc_run_inplace( fr.data(), sz.data(), fr.size(), batch, 1UL << 16, (int)depth, ring, &si, di );
     if( !r && (si.hash != st.hash || si.pub_cnt != st.pub_cnt) ) r = 30;
     for( unsigned long c=0; !r && c<FD_VERIFY_TILE_DIAG_CNT; c++ )
-      if( c != FD_VERIFY_TILE_DIAG_BATCH_CNT && di[c] != diag[c] ) r = 31;
+      if( c != FD_VERIFY_TILE_DIAG_BATCH_CNT && c != FD_VERIFY_TILE_DIAG_AGE_CNT && di[c] != diag[c] ) r = 31;
   }
   for( unsigned char * p : fr ) free( p );
   if( r ) __builtin_trap();

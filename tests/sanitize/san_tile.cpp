@@ -53,7 +53,7 @@ int main( int argc, char ** argv ) {
       int ri = tc_run_inplace( fr.data(), sz.data(), n, bsigs[k], mblob[k], 2 + k, rings[k], &si, di );
       int same = si.pub_cnt == st.pub_cnt && si.hash == st.hash;
       for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ )
-        if( c != FD_VERIFY_TILE_DIAG_BATCH_CNT ) same &= di[c] == diag[c];
+        if( c != FD_VERIFY_TILE_DIAG_BATCH_CNT && c != FD_VERIFY_TILE_DIAG_AGE_CNT ) same &= di[c] == diag[c];
       printf( "{\"pass\": \"inplace%d\", \"rc\": %d, \"ring\": %lu, \"pub_cnt\": %lu, \"batches\": %lu, \"same\": %d}\n",
               k, ri, rings[k], si.pub_cnt, di[FD_VERIFY_TILE_DIAG_BATCH_CNT], same );
       if( ri ) return 40 + ri;

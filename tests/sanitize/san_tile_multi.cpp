@@ -165,7 +165,7 @@ int main( int argc, char ** argv ) {
     fd_ed25519_gpu_t * g[2];
     for( int e=0; e<2; e++ ) g[e] = fd_ed25519_gpu_new_ex( e, 128, 8UL << 20, 2 );
     fake_engine_speed( g[0], ns0 ); fake_engine_speed( g[1], ns0 * 5 / 4 );
-    fd_verify_tile_cfg_t cfg = { 128UL, 16UL, 64UL };
+    fd_verify_tile_cfg_t cfg = { 128UL, 16UL, 64UL, -1L };   /* full batches only: the split is the point */
     tc_state s4; memset( &s4, 0, sizeof(s4) ); s4.hash = 1469598103934665603UL;
     fd_verify_tile_t * t = fd_verify_tile_new_multi( g, 2, &cfg, tc_pub, &s4 );
     CHECK( t );

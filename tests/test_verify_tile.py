@@ -213,7 +213,9 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob, engines):
     order = list(range(len(second), len(lay))) + list(range(len(second)))
     es = [fa.Engine(0, batch_sigs, max_blob, depth=3 if engines == 1 else 2) for _ in range(engines)]
     try:
-        tile = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region)
+        # max_wait_ns=-1: batches close on size only, so the two layouts below
+        # can be compared batch for batch (the wait bound is timing-dependent)
+        tile = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region, max_wait_ns=-1)
         o, s_ = off[order], sz[order]
         for a in range(0, len(order), 97):                 # bursts, with housekeeping between
             tile.rx_burst(region, o[a:a + 97], s_[a:a + 97], ctl=np.arange(a, min(a + 97, len(order)), dtype=np.uint64))
@@ -245,7 +247,7 @@ def test_tile_inplace_vs_reference(ref, batch_sigs, max_blob, engines):
         sz2 = np.array([len(f) for f in lay2], np.uint32)
         off2 = np.concatenate([[0], np.cumsum(sz2)[:-1]]).astype(np.uint64)
         region2 = np.frombuffer(b"".join(lay2) + b"\0" * 64, np.uint8).copy()
-        tile2 = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region2)
+        tile2 = VerifyTile(es[0] if engines == 1 else es, batch_sigs=batch_sigs, region=region2, max_wait_ns=-1)
         for a in range(0, len(lay2), 97):
             tile2.rx_burst(region2, off2[a:a + 97], sz2[a:a + 97], ctl=np.arange(a, min(a + 97, len(lay2)), dtype=np.uint64))
             tile2.service()

@@ -1,0 +1,109 @@
+"""The verify tile task run the way a validator runs it (VERDICT r05 items
+1, 2): fd_verify_tile_task.run on its own thread, fed by a live producer
+thread over an mcache/dcache link shaped like the reference's QUIC ->
+verify link (tests/vt_live.cpp), no fd_verify_tile_service call from
+outside the run loop and HALT only at the end.
+
+  - liveness (the reference verifies and publishes each frag as it
+    arrives, src/app/frank/load/fd_frank_verify_synth_load.c:378-410,
+    inside a run loop that never returns, src/app/frank/fd_frank_verify.c:
+    139-204): at 1 frag/ms and at 1,000 frags/ms every frag is published
+    within 2 ms of its receipt, before HALT, and the publish set equals
+    the reference's per-frag semantics (its tcache and fd_ed25519_verify);
+  - overrun safety (the link has no credits, src/app/fdctl/config/
+    default.toml:473-477; consumers re-check a frag's seq after using it,
+    src/disco/dedup/fd_dedup.c:512-522): an in-place tile on a 16,384-frag
+    dcache with 65,536-signature batches, under a producer that laps it,
+    never publishes a frag whose bytes differ from the bytes the producer
+    wrote for that seq and never deadlocks; with a producer that honours
+    fd_verify_tile_held it publishes exactly the reference's set."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, oracle_batch
+from live_common import expected_cyclic, read_pubout, run, write_frags
+from test_verify_tile import expected_for, make_stream
+
+EXE = os.path.join(ROOT, "firedancer_amd", "vt_live")
+
+
+def _exe():
+    assert os.path.exists(EXE), "build with make -C firedancer_amd"
+    return EXE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["copy", "inplace"])
+@pytest.mark.parametrize("rate,n_sigs", [(1000, 3000), (1_000_000, 200_000)], ids=["1_per_ms", "1000_per_ms"])
+def test_task_live_producer_bounded_latency(ref, tmp_path, mode, rate, n_sigs):
+    frags = make_stream(n_sigs, 5 + n_sigs % 97, ref)
+    exp_pub, exp, nsig = expected_for(frags, ref)
+    p, po = str(tmp_path / "frags.bin"), str(tmp_path / "pub.bin")
+    write_frags(p, frags)
+    d = run(_exe(), p, mode=mode, rate=rate, count=len(frags), depth=16384, batch=4096, eng_depth=8, pubout=po,
+            timeout=240)
+    assert d["rc"] == 0 and d["booted"] == 1 and d["err"] == 0, d
+    # nothing overran: every frag was taken, in order
+    assert d["taken"] == len(frags) and d["ovrnp"] == 0 and d["ovrnr"] == 0 and d["diag"]["OVRN_CNT"] == 0, d
+    pub = read_pubout(po)
+    # the publish set: the reference's, in arrival order, every byte intact
+    assert [frags[int(s)] for s in pub[:, 0]] == [f for _, f in exp_pub]
+    assert d["mismatch"] == 0 and d["order_err"] == 0
+    for k, v in exp.items():
+        assert d["diag"][k] == v, k
+    assert d["diag"]["SIG_CNT"] == nsig
+    # liveness: all of it before HALT, each within 2 ms of its receipt
+    assert d["pub_before_halt"] == len(exp_pub), d
+    lat_ms = pub[:, 1] / 1e6
+    assert lat_ms.max() <= 2.0, (float(lat_ms.max()), float(np.percentile(lat_ms, 99)), d["lat"])
+    print(f"{mode} {rate}/s: {len(exp_pub)} published, p50 {np.median(lat_ms):.3f} ms, "
+          f"p99 {np.percentile(lat_ms, 99):.3f} ms, max {lat_ms.max():.3f} ms, batches {d['diag']['BATCH_CNT']} "
+          f"(wait-bound closes {d['diag']['AGE_CNT']})")
+
+
+def _cyclic_corpus(ref, n_sigs, seed):
+    from firedancer_amd import corpus, txn
+    b = corpus.solana_txns(n_sigs, seed=seed, sig_dist=[1 / 12] * 12, nthreads=16)
+    starts = sorted({int(dd["sig_off"]) // corpus.TXN_MTU * corpus.TXN_MTU for dd in b.desc})
+    pay = [bytearray(b.blob[s:s + corpus.TXN_MTU]) for s in starts]
+    rng = np.random.default_rng(seed)
+    for q in pay:                               # ~10% txns with one corrupted signature
+        if rng.random() < 0.10:
+            j = int(rng.integers(0, q[0]))
+            q[1 + 64 * j + int(rng.integers(8, 64))] ^= 1 << int(rng.integers(0, 8))
+    frags = [txn.frag(bytes(q)) for q in pay]
+    return frags, expected_cyclic(frags, ref, oracle_batch)
+
+
+@pytest.mark.gpu
+def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
+    """16,384-frag dcache, 65,536-signature batches, a producer that runs
+    free (as the reference's QUIC tile does): frags lapped before their
+    batch publishes are dropped (OVRN_CNT), the rest publish with exactly
+    the bytes the producer wrote for their seq and only if the reference
+    publishes them; then the same link with a producer honouring
+    fd_verify_tile_held: no overrun, no deadlock (the span-half and wait
+    bound close batches the dcache cannot fill), the reference's set."""
+    frags, ok = _cyclic_corpus(ref, 20000, 71)
+    assert 0 < ok.sum() < len(ok)
+    p = str(tmp_path / "frags.bin")
+    write_frags(p, frags)
+    ex = str(tmp_path / "expect.bin")
+    ok.astype(np.uint8).tofile(ex)
+    n = 200_000
+    free = run(_exe(), p, mode="inplace", rate=0, count=n, depth=16384, batch=65536, eng_depth=3, expect=ex, timeout=240)
+    assert free["rc"] == 0 and free["booted"] == 1, free
+    assert free["mismatch"] == 0 and free["false_pub"] == 0 and free["order_err"] == 0, free
+    assert free["pub"] <= free["taken_pass_expected"]
+    acc = sum(free["diag"][k] for k in ("PUB_CNT", "SV_FILT_CNT", "HA_FILT_CNT", "BAD_CNT", "OVRN_CNT"))
+    assert acc == free["taken"], free
+    print("free-running producer:", {k: free[k] for k in ("produced", "taken", "pub", "ovrnp", "ovrnr")},
+          "OVRN_CNT", free["diag"]["OVRN_CNT"], "batches", free["diag"]["BATCH_CNT"])
+    cred = run(_exe(), p, mode="inplace", rate=0, count=n, depth=16384, batch=65536, eng_depth=3, expect=ex, credit=1,
+               timeout=240)
+    assert cred["rc"] == 0 and cred["booted"] == 1, cred
+    assert cred["taken"] == n and cred["ovrnp"] == 0 and cred["ovrnr"] == 0 and cred["diag"]["OVRN_CNT"] == 0, cred
+    assert cred["mismatch"] == 0 and cred["false_pub"] == 0 and cred["pub"] == cred["taken_pass_expected"], cred
+    assert cred["pub_before_halt"] == cred["pub"]
