@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
         L.fd_ed25519_gpu_max_sigs.restype = ul
         L.fd_ed25519_gpu_max_blob.argtypes = [vp]
         L.fd_ed25519_gpu_max_blob.restype = ul
+        L.fd_ed25519_gpu_verify_ptrs.argtypes = [vp, ul, vp, vp, vp, vp, vp]
+        L.fd_ed25519_gpu_verify_ptrs.restype = ip
         L.fd_ed25519_gpu_stage.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
         L.fd_ed25519_gpu_stage.restype = ip
         L.fd_ed25519_gpu_unstage.argtypes = [vp, vp]
@@ -286,6 +288,24 @@ class Engine:
         if err:
             raise EngineError(f"verify_packed: {strerror(err)}: {last_error()}")
         return out
+
+    def verify_ptrs(self, msgs, sigs, pubs) -> tuple[int, np.ndarray]:
+        """fd_ed25519_gpu_verify_ptrs: fd_ed25519_verify_batch on this engine,
+        messages of any length (past max_blob: the long path)."""
+        n = len(msgs)
+        keep = [m if isinstance(m, np.ndarray) else np.frombuffer(bytes(m), np.uint8) for m in msgs]
+        sb = [ctypes.create_string_buffer(bytes(x), 64) for x in sigs]
+        pb = [ctypes.create_string_buffer(bytes(x), 32) for x in pubs]
+        MP = ctypes.c_void_p * max(n, 1)
+        mp = MP(*[m.ctypes.data if len(m) else None for m in keep])
+        sp = MP(*[ctypes.cast(b, ctypes.c_void_p) for b in sb])
+        pp = MP(*[ctypes.cast(b, ctypes.c_void_p) for b in pb])
+        sz = (ctypes.c_ulong * max(n, 1))(*[len(m) for m in keep])
+        out = np.zeros(n, dtype=np.int32)
+        r = lib().fd_ed25519_gpu_verify_ptrs(self._h, n, mp, sz, sp, pp, _p(out))
+        if r in (ERR_ARG, ERR_GPU):
+            raise EngineError(f"verify_ptrs: {strerror(r)}: {last_error()}")
+        return r, out
 
     def verify_dev(self, n: int, d_blob: int, blob_sz: int, d_desc: int, d_out: int, stream: int = 0,
                    inputs_ready: bool = False) -> None:

@@ -1137,7 +1137,7 @@ extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long
 static std::mutex          fd_default_lock;
 static fd_ed25519_gpu_t *  fd_default_gpu = NULL;
 static unsigned long       fd_default_sigs = 1UL << 16;
-static unsigned long       fd_default_blob = 1UL << 26;
+static unsigned long       fd_default_blob = 1UL << 26;   /* $FD_ED25519_GPU_DEFAULT_BLOB overrides */
 
 static fd_ed25519_gpu_t * fd_default_engine( void );
 extern "C" fd_ed25519_gpu_t * fd_ed25519_gpu_default( void ) { return fd_default_engine(); }
@@ -1180,7 +1180,10 @@ static fd_ed25519_gpu_t * fd_default_engine( void ) {
   std::lock_guard<std::mutex> guard( fd_default_lock );
   if( !fd_default_gpu ) {
     char const * dev = getenv( "FD_ED25519_GPU_DEVICE" );
-    fd_default_gpu = fd_ed25519_gpu_new_ex( dev ? atoi( dev ) : 0, fd_default_sigs, fd_default_blob, fd_vq_leaders() );
+    char const * bl  = getenv( "FD_ED25519_GPU_DEFAULT_BLOB" );   /* staging blob bytes (messages above it take the long path) */
+    unsigned long blob = bl ? strtoul( bl, NULL, 0 ) : fd_default_blob;
+    if( blob < 4096UL ) blob = 4096UL;
+    fd_default_gpu = fd_ed25519_gpu_new_ex( dev ? atoi( dev ) : 0, fd_default_sigs, blob, fd_vq_leaders() );
     static int fini_set = 0;
     if( fd_default_gpu && !fini_set ) { fini_set = 1; atexit( fd_default_engine_fini ); }
   }
@@ -1202,23 +1205,175 @@ static int fd_stage_wait( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_des
   return 0;
 }
 
+/* ---- Long messages ------------------------------------------------------
+
+   The reference verifies a message of any length: fd_sha512_append streams
+   it (src/ballet/sha512/fd_sha512.c:282-349; fd_ed25519.h:96-101 bounds
+   nothing).  A message too large for one staging blob (or for a 32-bit
+   descriptor) is verified here without CPU crypto: the padded byte stream
+   R || A || M || 0x80 || 0.. || bitlen is moved through a staged slot's
+   pinned blob in pieces, each piece hashed on the device into a chaining
+   state that stays in the slot's HBM between launches
+   (fd_k_sha512_stream, one lane per message, several messages side by
+   side), then the signatures run prep (digest from the state), point
+   decompression and the uniform DSM (fd_ed25519_gpu_launch_long) -- the
+   same code path bit for bit as any other batch after the hash.  SHA-512
+   is serial within a message: one lane hashes ~1 GB/s / 64, so this is
+   correct for any length but slow for very long messages. */
+struct fd_long_req { uint8_t const * sig; uint8_t const * pub; uint8_t const * msg; unsigned long sz; };
+
+/* bytes [pos, pos+len) of request r's padded SHA-512 input stream */
+static void fd_long_pack( uint8_t * dst, fd_long_req const & r, unsigned long pos, unsigned long len ) {
+  unsigned long T = 64UL + r.sz;                            /* R || A || M */
+  unsigned long P = ( T + 17UL + 127UL ) & ~127UL;          /* padded */
+  unsigned long x = pos, end = pos + len;
+  if( x < 32UL && x < end ) { unsigned long k = ( end < 32UL ? end : 32UL ) - x; memcpy( dst, r.sig + x, k ); dst += k; x += k; }
+  if( x < 64UL && x < end ) { unsigned long k = ( end < 64UL ? end : 64UL ) - x; memcpy( dst, r.pub + (x - 32UL), k ); dst += k; x += k; }
+  if( x < T && x < end )    { unsigned long k = ( end < T ? end : T ) - x;       memcpy( dst, r.msg + (x - 64UL), k ); dst += k; x += k; }
+  if( x < end ) {
+    memset( dst, 0, end - x );
+    if( x == T ) dst[0] = 0x80;                             /* the padding bit */
+    if( end == P ) {                                        /* the 128-bit big-endian bit count ends the stream */
+      uint8_t * L = dst + ( end - x ) - 16;
+      unsigned long hi = T >> 61, lo = T << 3;
+      for( int b=0; b<8; b++ ) { L[7-b] = (uint8_t)(hi >> (8*b)); L[15-b] = (uint8_t)(lo >> (8*b)); }
+    }
+  }
+}
+
+/* the staged slot owning blob (the caller holds the stage) */
+static fd_ed25519_gpu_slot * fd_slot_of( fd_ed25519_gpu_t * g, void const * blob ) {
+  std::lock_guard<std::mutex> guard( g->lock );
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) return &g->slot[s];
+  return NULL;
+}
+
+/* wait for the staged slot's queued work; on a timeout the slot is given
+   up (orphaned: reclaimed once its event fires) instead of reused */
+static int fd_long_wait( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl ) {
+  hipError_t e = hipEventRecord( sl->done, sl->stream );
+  if( e != hipSuccess ) return fd_gpu_fail( "long: event", e );
+  int err = fd_event_wait( sl->done, fd_timeout( g ) );
+  if( err ) {
+    std::lock_guard<std::mutex> guard( g->lock );
+    sl->ticket = g->next_ticket++; sl->orphan = 1; sl->staged = 0;
+  }
+  return err;
+}
+
+static int fd_run_long( fd_ed25519_gpu_t * g, unsigned long cnt, fd_long_req const * rq, int * out ) {
+  void * vb; fd_ed25519_gpu_desc_t * dd;
+  int err = fd_stage_wait( g, &vb, &dd );
+  if( err ) return err;
+  fd_ed25519_gpu_slot * sl = fd_slot_of( g, vb );
+  if( !sl ) { fd_ed25519_gpu_unstage( g, vb ); return FD_ED25519_ERR_GPU; }
+  hipError_t e = hipSetDevice( g->device );
+  if( e != hipSuccess ) { fd_ed25519_gpu_unstage( g, vb ); return fd_gpu_fail( "hipSetDevice", e ); }
+  int mode = fd_knobs_get( g ).mode;
+  uint64_t * d_st = (uint64_t *)sl->work.fin;              /* 160 B of scratch per signature >= the 64 B state */
+  /* messages per group: each needs >= one 128-byte block and a 16-byte
+     piece entry per launch, and its 96 bytes of R || S || A after */
+  unsigned long G = g->max_blob / 256UL;
+  if( G > g->max_sigs ) G = g->max_sigs;
+  if( G > 4096UL ) G = 4096UL;
+  if( !G ) { fd_ed25519_gpu_unstage( g, vb ); return FD_ED25519_ERR_ARG; }
+  for( unsigned long i0=0; i0<cnt && !err; i0+=G ) {
+    unsigned long m = cnt - i0 < G ? cnt - i0 : G;
+    /* blocks per message per launch, the piece table after the data */
+    unsigned long C = ( g->max_blob - m * sizeof(fd_sha_piece_t) ) / ( m * 128UL );
+    unsigned long toff = m * C * 128UL;
+    std::vector<unsigned long> pos( m, 0UL );
+    for(;;) {
+      fd_sha_piece_t * pc = (fd_sha_piece_t *)( sl->h_blob + toff );
+      int more = 0;
+      for( unsigned long j=0; j<m; j++ ) {
+        fd_long_req const & r = rq[ i0 + j ];
+        unsigned long P = ( 64UL + r.sz + 17UL + 127UL ) & ~127UL;
+        unsigned long nb = ( P - pos[j] ) / 128UL;
+        if( nb > C ) nb = C;
+        pc[j].off = j * C * 128UL; pc[j].nblk = (uint32_t)nb; pc[j].first = pos[j] == 0UL;
+        if( nb ) { fd_long_pack( sl->h_blob + j * C * 128UL, r, pos[j], nb * 128UL ); pos[j] += nb * 128UL; more = 1; }
+      }
+      if( !more ) break;
+      if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, toff + m * sizeof(fd_sha_piece_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess
+       || (e = fd_ed25519_gpu_launch_sha512_stream( (uint32_t)m, d_st, sl->d_blob, (fd_sha_piece_t const *)( sl->d_blob + toff ), sl->stream )) != hipSuccess ) {
+        err = fd_gpu_fail( "long: hash piece", e ); break;
+      }
+      if( (err = fd_long_wait( g, sl )) ) return err;       /* the pinned blob is reused next round */
+    }
+    if( err ) break;
+    /* the signatures: R || S || A per message, descriptors after */
+    unsigned long bsz = 96UL * m, doff = fd_desc_off( bsz );
+    fd_ed25519_gpu_desc_t * hd = (fd_ed25519_gpu_desc_t *)( sl->h_blob + doff );
+    for( unsigned long j=0; j<m; j++ ) {
+      memcpy( sl->h_blob + 96UL*j, rq[ i0 + j ].sig, 64 );
+      memcpy( sl->h_blob + 96UL*j + 64UL, rq[ i0 + j ].pub, 32 );
+      hd[j].sig_off = (uint32_t)(96UL*j); hd[j].pub_off = (uint32_t)(96UL*j + 64UL); hd[j].msg_off = 0; hd[j].msg_sz = 0;
+    }
+    memset( sl->h_blob + bsz, 0, doff - bsz );
+    if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + m * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, sl->stream )) != hipSuccess
+     || (e = fd_ed25519_gpu_launch_long( m, sl->d_blob, bsz, (fd_ed25519_gpu_desc_t const *)( sl->d_blob + doff ), d_st, &sl->work,
+                                         sl->d_out, sl->stream, mode )) != hipSuccess
+     || (e = hipMemcpyAsync( sl->h_out, sl->d_out, m * sizeof(int32_t), hipMemcpyDeviceToHost, sl->stream )) != hipSuccess ) {
+      err = fd_gpu_fail( "long: verify", e ); break;
+    }
+    if( (err = fd_long_wait( g, sl )) ) return err;
+    for( unsigned long j=0; j<m; j++ ) out[ i0 + j ] = sl->h_out[j];
+  }
+  if( err ) (void)hipStreamSynchronize( sl->stream );      /* a failed enqueue: what was queued drains before the slot is lent again */
+  fd_ed25519_gpu_unstage( g, vb );
+  return err;
+}
+
 /* Pack pointer-array inputs into a pinned slot blob in chunks of the
    engine capacity and run them: each chunk is staged in a free slot's
    pinned buffers, submitted and waited on through the ring (stage /
    try_submit / poll), so the engine lock is held only to take the slot,
    enqueue and collect -- never across the device round trip -- and
    callers on other threads run their batches on the other slots at the
-   same time (fd_ed25519_verify's group-commit leaders). */
-static int fd_run_ptr_batch( unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
+   same time (fd_ed25519_verify's group-commit leaders).  Messages too long
+   for a staging blob (or a 32-bit descriptor) take the long path. */
+static int fd_run_ptr_short( fd_ed25519_gpu_t * g, unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
+                             uint8_t const * shared_msg, unsigned long shared_sz,
+                             uint8_t const * const * sigp, uint8_t const (*siga)[64],
+                             uint8_t const * const * pubp, uint8_t const (*puba)[32], int * out );
+
+static int fd_run_ptr_batch( fd_ed25519_gpu_t * g, unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
                              uint8_t const * shared_msg, unsigned long shared_sz,
                              uint8_t const * const * sigp, uint8_t const (*siga)[64],
                              uint8_t const * const * pubp, uint8_t const (*puba)[32], int * out ) {
-  fd_ed25519_gpu_t * g = fd_default_engine();
   if( !g ) return FD_ED25519_ERR_GPU;
-  /* every message must fit one engine blob: checked before any chunk runs,
-     so ERR_ARG writes nothing (fd_ed25519_gpu.h) */
-  if( shared_msg ) { if( shared_sz > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG; }
-  else for( unsigned long k=0; k<n; k++ ) if( msg_sz[k] > 0x7fffffffUL || msg_sz[k] > g->max_blob - 96UL ) return FD_ED25519_ERR_ARG;
+  unsigned long const lim = g->max_blob > 96UL ? g->max_blob - 96UL : 0UL;
+  if( shared_msg ) {
+    if( shared_sz <= lim && shared_sz <= 0x7fffffffUL ) return fd_run_ptr_short( g, n, NULL, NULL, shared_msg, shared_sz, sigp, siga, pubp, puba, out );
+    std::vector<fd_long_req> rq( n );
+    for( unsigned long k=0; k<n; k++ ) rq[k] = { sigp ? sigp[k] : siga[k], pubp ? pubp[k] : puba[k], shared_msg, shared_sz };
+    return fd_run_long( g, n, rq.data(), out );
+  }
+  unsigned long nl = 0;
+  for( unsigned long k=0; k<n; k++ ) nl += msg_sz[k] > lim || msg_sz[k] > 0x7fffffffUL;
+  if( !nl ) return fd_run_ptr_short( g, n, msg, msg_sz, NULL, 0, sigp, siga, pubp, puba, out );
+  /* split: the short ones through the ring as usual, the long ones after */
+  std::vector<uint8_t const *> sm, ss, sp; std::vector<unsigned long> sz, si, li;
+  std::vector<fd_long_req> rq;
+  for( unsigned long k=0; k<n; k++ ) {
+    uint8_t const * s = sigp ? sigp[k] : siga[k], * p = pubp ? pubp[k] : puba[k];
+    if( msg_sz[k] > lim || msg_sz[k] > 0x7fffffffUL ) { rq.push_back( { s, p, msg[k], msg_sz[k] } ); li.push_back( k ); }
+    else { sm.push_back( msg[k] ); sz.push_back( msg_sz[k] ); ss.push_back( s ); sp.push_back( p ); si.push_back( k ); }
+  }
+  std::vector<int> o( n );
+  int err = si.empty() ? 0 : fd_run_ptr_short( g, si.size(), sm.data(), sz.data(), NULL, 0, ss.data(), NULL, sp.data(), NULL, o.data() );
+  if( err ) return err;
+  for( unsigned long j=0; j<si.size(); j++ ) out[ si[j] ] = o[j];
+  if( (err = fd_run_long( g, rq.size(), rq.data(), o.data() )) ) return err;
+  for( unsigned long j=0; j<li.size(); j++ ) out[ li[j] ] = o[j];
+  return 0;
+}
+
+static int fd_run_ptr_short( fd_ed25519_gpu_t * g, unsigned long n, uint8_t const * const * msg, unsigned long const * msg_sz,
+                             uint8_t const * shared_msg, unsigned long shared_sz,
+                             uint8_t const * const * sigp, uint8_t const (*siga)[64],
+                             uint8_t const * const * pubp, uint8_t const (*puba)[32], int * out ) {
   unsigned long i = 0;
   while( i < n ) {
     void * vb; fd_ed25519_gpu_desc_t * dd;
@@ -1269,9 +1424,21 @@ extern "C" int fd_ed25519_verify_batch( unsigned long n, uint8_t const * const *
   if( !n ) return 0;
   if( !msg || !msg_sz || !sig || !pub || !out_err ) return FD_ED25519_ERR_ARG;
   for( unsigned long i=0; i<n; i++ ) if( !sig[i] || !pub[i] || (msg_sz[i] && !msg[i]) ) return FD_ED25519_ERR_ARG;
-  int err = fd_run_ptr_batch( n, msg, msg_sz, NULL, 0, sig, NULL, pub, NULL, out_err );
+  int err = fd_run_ptr_batch( fd_default_engine(), n, msg, msg_sz, NULL, 0, sig, NULL, pub, NULL, out_err );
   if( err ) return err;
   return fd_first_err( n, out_err );
+}
+
+extern "C" int fd_ed25519_gpu_verify_ptrs( fd_ed25519_gpu_t * g, unsigned long n, uint8_t const * const * msg,
+                                           unsigned long const * msg_sz, uint8_t const * const * sig,
+                                           uint8_t const * const * pub, int * out ) {
+  if( !g ) return FD_ED25519_ERR_ARG;
+  if( !n ) return 0;
+  if( !msg || !msg_sz || !sig || !pub || !out ) return FD_ED25519_ERR_ARG;
+  for( unsigned long i=0; i<n; i++ ) if( !sig[i] || !pub[i] || (msg_sz[i] && !msg[i]) ) return FD_ED25519_ERR_ARG;
+  int err = fd_run_ptr_batch( g, n, msg, msg_sz, NULL, 0, sig, NULL, pub, NULL, out );
+  if( err ) return err;
+  return fd_first_err( n, out );
 }
 
 extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned long msg_sz, uint8_t const (*sig)[64],
@@ -1282,7 +1449,7 @@ extern "C" int fd_ed25519_verify_batch_single_msg( uint8_t const * msg, unsigned
   int * tmp = NULL;
   if( !out ) { tmp = (int *)malloc( n * sizeof(int) ); if( !tmp ) return FD_ED25519_ERR_GPU; out = tmp; }
   static uint8_t const empty[1] = { 0 };
-  int err = fd_run_ptr_batch( n, NULL, NULL, msg_sz ? msg : empty, msg_sz, NULL, sig, NULL, pub, out );
+  int err = fd_run_ptr_batch( fd_default_engine(), n, NULL, NULL, msg_sz ? msg : empty, msg_sz, NULL, sig, NULL, pub, out );
   int r = err ? err : fd_first_err( n, out );
   free( tmp );
   return r;
@@ -1312,16 +1479,15 @@ static void fd_vq_run( std::vector<fd_vreq *> const & b, std::vector<int> & code
   unsigned long n = b.size();
   std::vector<uint8_t const *> m, s, p; std::vector<unsigned long> sz; std::vector<unsigned long> idx;
   fd_ed25519_gpu_t * g = fd_default_engine();
-  unsigned long lim = g ? fd_ed25519_gpu_max_blob( g ) - 96UL : 0UL;
   code.assign( n, FD_ED25519_ERR_GPU );
   for( unsigned long k=0; k<n; k++ ) {
     fd_vreq const * r = b[k];
-    if( !r->s || !r->p || (r->sz && !r->m) || (g && (r->sz > lim || r->sz > 0x7fffffffUL)) ) { code[k] = FD_ED25519_ERR_ARG; continue; }
+    if( !r->s || !r->p || (r->sz && !r->m) ) { code[k] = FD_ED25519_ERR_ARG; continue; }
     m.push_back( r->m ); s.push_back( r->s ); p.push_back( r->p ); sz.push_back( r->sz ); idx.push_back( k );
   }
   if( idx.empty() ) return;
   std::vector<int> out( idx.size() );
-  int err = fd_run_ptr_batch( idx.size(), m.data(), sz.data(), NULL, 0, s.data(), NULL, p.data(), NULL, out.data() );
+  int err = fd_run_ptr_batch( g, idx.size(), m.data(), sz.data(), NULL, 0, s.data(), NULL, p.data(), NULL, out.data() );
   for( unsigned long j=0; j<idx.size(); j++ ) code[idx[j]] = err ? err : out[j];
 }
 

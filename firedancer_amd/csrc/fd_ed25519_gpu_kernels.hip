@@ -151,11 +151,16 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 #define FD_PREP_WG 256
 #endif
 
+/* DIG 1 (fd_k_prep_dig, long messages): the digest of R || A || M comes
+   from dig_in (the SHA-512 chaining state streamed through
+   fd_k_sha512_stream, [n][8] words) instead of being hashed here; DIG 0
+   is the ring / resident path's fd_k_prep */
+template<int DIG>
 static __device__ __forceinline__ void
-fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
-              fd_ed25519_gpu_desc_t const * __restrict__ desc,
-              int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-              fd_lds_u8 * sha_stage, uint64_t * __restrict__ kout, int sigmajor ) {
+fd_prep_body_t( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+                fd_ed25519_gpu_desc_t const * __restrict__ desc,
+                int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
+                fd_lds_u8 * sha_stage, uint64_t * __restrict__ kout, int sigmajor, uint64_t const * __restrict__ dig_in ) {
   if( i >= n ) return;
   fd_ed25519_gpu_desc_t d = desc[i];
   /* a descriptor outside the blob is reported, never dereferenced (the
@@ -187,7 +192,12 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
   if( st != FD_ST_PENDING ) { op_start[i] = FD_OPS_MAX; return; }
 
   uint64_t dig[8];
-  fd_sha512_ram( dig, R, A, M, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
+  if( DIG ) {
+#pragma unroll
+    for( int j=0; j<8; j++ ) dig[j] = fd_bswap64( dig_in[8*i + (uint64_t)j] );
+  } else {
+    fd_sha512_ram( dig, R, A, M, d.msg_sz, sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES );
+  }
   uint64_t k[4];
   fd_sc_reduce( k, dig );
   if( kout ) {   /* diagnostics (fd_ed25519_gpu_debug_k): k = SHA-512(R||A||M) mod L, [4][n] */
@@ -229,6 +239,14 @@ fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_
   lds_u16 * slots = (lds_u16 *)(sha_stage + (threadIdx.x >> 6)*FD_SHA_STAGE_BYTES) + (threadIdx.x & 63u);
   op_start[i] = sigmajor ? fd_recode2( sw, kw, ops + i*FD_OPS_MAX, 1, slots, 64u )
                          : fd_recode2( sw, kw, ops + i, n, slots, 64u );
+}
+
+static __device__ __forceinline__ void
+fd_prep_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
+              fd_ed25519_gpu_desc_t const * __restrict__ desc,
+              int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
+              fd_lds_u8 * sha_stage, uint64_t * __restrict__ kout, int sigmajor ) {
+  fd_prep_body_t<0>( i, n, blob, blob_sz, desc, status, ops, op_start, strict, sha_stage, kout, sigmajor, NULL );
 }
 
 /* fd_prep_body on a wave pair (the latency path's front end, fd_k_front):
@@ -2177,6 +2195,80 @@ extern "C" hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * 
   if( !n ) return hipSuccess;
   hipLaunchKernelGGL( fd_k_sha512_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                       n, blob, desc, (uint64_t *)out, is384 );
+  return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------ */
+/* Long messages (fd_ed25519_gpu_private.h): SHA-512 streamed through the
+   device in pieces, one lane per message, the chaining state kept in HBM
+   between launches (the reference hashes any length in one streaming
+   pass, fd_sha512_append, src/ballet/sha512/fd_sha512.c:282-349; the host
+   only moves the padded byte stream).  A lane fetches block b+1's 128
+   bytes while it compresses block b. */
+
+extern "C" __global__ void __launch_bounds__(64)
+fd_k_sha512_stream( uint32_t n, uint64_t * __restrict__ st, uint8_t const * __restrict__ data,
+                    fd_sha_piece_t const * __restrict__ pc ) {
+  uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if( i >= n ) return;
+  fd_sha_piece_t p = pc[i];
+  if( !p.nblk ) return;
+  uint64_t s[8];
+#pragma unroll
+  for( int j=0; j<8; j++ ) s[j] = p.first ? fd_gpu_sha512_iv[0][j] : st[8u*i + (uint32_t)j];
+  ulonglong2 const * q = (ulonglong2 const *)(data + p.off);
+  ulonglong2 cur[8];
+#pragma unroll
+  for( int c=0; c<8; c++ ) cur[c] = q[c];
+  for( uint32_t b=0; b<p.nblk; b++ ) {
+    uint64_t w[16];
+#pragma unroll
+    for( int c=0; c<8; c++ ) { w[2*c] = fd_bswap64( cur[c].x ); w[2*c+1] = fd_bswap64( cur[c].y ); }
+    if( b + 1u < p.nblk ) {
+      q += 8;
+#pragma unroll
+      for( int c=0; c<8; c++ ) cur[c] = q[c];
+    }
+    fd_sha512_compress( s, w );
+  }
+#pragma unroll
+  for( int j=0; j<8; j++ ) st[8u*i + (uint32_t)j] = s[j];
+}
+
+/* fd_k_prep with the digests from the stream's chaining states */
+extern "C" __global__ void __launch_bounds__(256)
+fd_k_prep_dig( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * __restrict__ desc,
+               uint64_t const * __restrict__ dig, int32_t * __restrict__ status, uint8_t * __restrict__ ops,
+               int32_t * __restrict__ op_start, int strict ) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4*FD_SHA_STAGE_BYTES];   /* the recoder's digit slots */
+  fd_prep_body_t<1>( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict,
+                     (fd_lds_u8 *)stage, NULL, 0, dig );
+}
+
+extern "C" hipError_t fd_ed25519_gpu_launch_sha512_stream( uint32_t n, uint64_t * st, uint8_t const * data,
+                                                           fd_sha_piece_t const * pieces, hipStream_t stream ) {
+  if( !n ) return hipSuccess;
+  hipLaunchKernelGGL( fd_k_sha512_stream, dim3((n + 63u) / 64u), dim3(64), 0, stream, n, st, data, pieces );
+  return hipGetLastError();
+}
+
+/* the rest of a long-message verify: prep from the digests, decompression,
+   then the uniform DSM (step-major op streams, its own Ai tables) */
+extern "C" hipError_t fd_ed25519_gpu_launch_long( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                                  uint64_t const * st, fd_ed25519_gpu_work_t const * w, int32_t * out,
+                                                  hipStream_t stream, int mode ) {
+  if( !n ) return hipSuccess;
+  mode &= 0xff;
+  int portable = mode == FD_ED25519_GPU_MODE_PORTABLE;
+  int strict   = mode == FD_ED25519_GPU_MODE_STRICT;
+  unsigned nb  = (unsigned)((n + 255) / 256);
+  unsigned nb2 = (unsigned)(((portable ? n : 2*n) + 255) / 256);
+  hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
+  if( e != hipSuccess ) return e;
+  hipLaunchKernelGGL( fd_k_prep_dig, dim3(nb), dim3(256), 0, stream, n, blob, blob_sz, desc, st, w->status, w->ops, w->op_start, strict );
+  hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
+  hipLaunchKernelGGL( fd_k_dsm, dim3(nb), dim3(256), 0, stream, n, w->status, w->pstat, w->pts, w->ops, w->op_start, w->tab, out,
+                      blob, desc, portable, strict );
   return hipGetLastError();
 }
 

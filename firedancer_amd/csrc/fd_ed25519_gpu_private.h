@@ -81,6 +81,20 @@ hipError_t fd_ed25519_gpu_launch_sha512( uint64_t n, uint8_t const * blob, fd_ed
 hipError_t fd_ed25519_gpu_launch( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
                                   fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream, int mode,
                                   uint64_t pool_min, uint64_t quad_max, uint64_t oct_max );
+/* Long messages (a message larger than one staging blob holds): the
+   SHA-512 of R || A || M streamed through the device in pieces.  One lane
+   per message: piece i compresses nblk consecutive 128-byte blocks of its
+   message's padded byte stream, staged at data + off, into the chaining
+   state st[8 i .. 8 i + 8) (the SHA-512 IV first if first != 0; nblk 0
+   leaves it unchanged).  fd_ed25519_gpu_launch_long then verifies n
+   signatures whose R || S and key lie in blob (descriptors as usual, the
+   message empty) with the digests taken from st instead of hashed. */
+typedef struct { uint64_t off; uint32_t nblk; uint32_t first; } fd_sha_piece_t;
+hipError_t fd_ed25519_gpu_launch_sha512_stream( uint32_t n, uint64_t * st, uint8_t const * data, fd_sha_piece_t const * pieces,
+                                                hipStream_t stream );
+hipError_t fd_ed25519_gpu_launch_long( uint64_t n, uint8_t const * blob, uint64_t blob_sz, fd_ed25519_gpu_desc_t const * desc,
+                                       uint64_t const * st, fd_ed25519_gpu_work_t const * w, int32_t * out, hipStream_t stream,
+                                       int mode );
 /* descriptor bounds: R||S, the key and the message inside blob[0, blob_sz)
    (64-bit sums, so no offset wraps) */
 static inline __host__ __device__ int fd_desc_in( fd_ed25519_gpu_desc_t const & d, uint64_t blob_sz ) {

@@ -32,9 +32,15 @@ extern "C" {
 /* ---- Per-signature API (replaces fd_ed25519.h:96-101) -----------------
 
    fd_ed25519_verify verifies one signature on the process-default
-   engine (device from $FD_ED25519_GPU_DEVICE, default 0).  sha is the
+   engine (device from $FD_ED25519_GPU_DEVICE, default 0; its staging blob
+   $FD_ED25519_GPU_DEFAULT_BLOB bytes, default 64 MiB).  sha is the
    reference's caller-owned fd_sha512_t scratch; it is accepted for ABI
-   compatibility and not touched.  msg==NULL is fine when sz==0. */
+   compatibility and not touched.  msg==NULL is fine when sz==0.  Like the
+   reference (fd_ed25519.h:96-101) it takes a message of any length: one
+   larger than the engine's staging blob is hashed on the device in
+   blob-sized pieces (the long path: SHA-512 chaining state kept in HBM
+   between pieces, then the usual decompression and DSM), serial within
+   the message -- correct at any length, slow for very long ones. */
 
 int
 fd_ed25519_verify( void const *  msg,
@@ -53,7 +59,8 @@ fd_ed25519_strerror( int err );
    msg_sz[i], sig[i], pub[i] ).  Returns 0 if every signature verified,
    else the first nonzero code in index order.  Returns
    FD_ED25519_ERR_ARG (and writes nothing) if n==0 with NULL arrays is
-   not the case and any array is NULL, or a msg_sz exceeds 2^31. */
+   not the case and any array is NULL.  Messages of any length (the long
+   path above for those past the staging blob). */
 
 int
 fd_ed25519_verify_batch( unsigned long           n,
@@ -65,7 +72,8 @@ fd_ed25519_verify_batch( unsigned long           n,
 
 /* fd_ed25519_verify_batch_single_msg: n signers over one shared message
    (vote-txn shape).  Returns 0 iff every element verifies, else the
-   first nonzero code in index order.  out_err_opt may be NULL. */
+   first nonzero code in index order.  out_err_opt may be NULL.  Any
+   message length. */
 
 int
 fd_ed25519_verify_batch_single_msg( uint8_t const * msg,
@@ -518,6 +526,19 @@ fd_ed25519_gpu_multi_verify_packed( fd_ed25519_gpu_multi_t *      multi,
                                     unsigned long                 blob_sz,
                                     fd_ed25519_gpu_desc_t const * desc,
                                     int *                         out );
+
+/* fd_ed25519_verify_batch on a given engine (not the process default):
+   pointer arrays in, out[i] each signature's code; messages of any length
+   (past the engine's staging blob: the long path).  Returns 0 if every
+   signature verified, else the first nonzero code in index order, or
+   FD_ED25519_ERR_ARG / FD_ED25519_ERR_GPU if the batch could not run. */
+int fd_ed25519_gpu_verify_ptrs( fd_ed25519_gpu_t *      gpu,
+                                unsigned long           n,
+                                uint8_t const * const * msg,
+                                unsigned long const *   msg_sz,
+                                uint8_t const * const * sig,
+                                uint8_t const * const * pub,
+                                int *                   out );
 
 /* Accept bitmap: bit i of bitmap[(n+7)/8] = (codes[i] == FD_ED25519_SUCCESS). */
 void fd_ed25519_codes_to_bitmap( unsigned long n, int const * codes, uint8_t * bitmap );
