@@ -19,10 +19,6 @@
 #ifndef FD_ED25519_GPU_FE_H
 #define FD_ED25519_GPU_FE_H
 
-#ifndef FD_FE_ADD_TWICE
-#define FD_FE_ADD_TWICE 1
-#endif
-
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -59,7 +55,7 @@ FD_DEV int64_t fd_opaque64( int64_t x ) {
    for both x*2 and x+x, which issues at half rate on gfx950
    (profiles/r02_ubench_int.txt).  Not volatile: unused results drop out. */
 FD_DEV int32_t fd_twice( int32_t x ) {
-#if defined(__HIP_DEVICE_COMPILE__) && FD_FE_ADD_TWICE
+#if defined(__HIP_DEVICE_COMPILE__)
   int32_t r;
   asm( "v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x) );
   return r;

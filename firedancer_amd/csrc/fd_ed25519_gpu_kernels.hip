@@ -132,24 +132,12 @@ FD_DEV void fd_ld32( uint32_t (&w)[8], uint8_t const * p ) {
 #include "fd_ed25519_gpu_wnaf.h"
 #include <atomic>
 
-/* FD_PREP_ZERO 1: fd_prep_body zeroes the step-major op column it owns
-   (rows FD_OPS_ZBASE..511) instead of a memset of the whole array before
-   the launch (0, the default).  Measured on one box
-   (profiles/r05_prep_zero_ab.jsonl): the prep itself runs 1.31 -> 1.26 ms
-   (its recoder's byte stores land on lines its zero stores just wrote),
-   but the pipelined step grows 15.78 -> 15.89 ms -- the zero stores run
-   beside the previous launch's pool, the memset's 0.1 ms does not hurt it
-   -- so the memset stays. */
-#ifndef FD_PREP_ZERO
-#define FD_PREP_ZERO 0
-#endif
-#define FD_OPS_ZBASE 144
-/* threads per fd_k_prep block (64: each wave's 9 KB stage freed when that
-   wave ends rather than when the slowest of four does; no faster, same
-   A/B) */
-#ifndef FD_PREP_WG
+/* The step-major op array is zeroed by a memset before fd_k_prep
+   (per-lane zeroing in the prep was measured and not adopted:
+   profiles/r05_prep_zero_ab.jsonl; the variant is kept as
+   profiles/r06_experiment_knobs.patch). */
+/* threads per fd_k_prep block (64-thread blocks measured no faster) */
 #define FD_PREP_WG 256
-#endif
 
 /* DIG 1 (fd_k_prep_dig, long messages): the digest of R || A || M comes
    from dig_in (the SHA-512 chaining state streamed through
@@ -221,17 +209,6 @@ fd_prep_body_t( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint6
 #pragma unroll
     for( int c=0; c<FD_OPS_MAX/16; c++ ) row[c] = make_int4( 0, 0, 0, 0 );
   }
-#if FD_PREP_ZERO
-  else {
-    /* step-major: this signature's column from t = FD_OPS_ZBASE on (a
-       stream starts at t >= 154, tests/test_quad_model.py; the DSMs read
-       from op_start on), one byte per row -- each row's 64 bytes of a wave
-       are one coalesced store.  Replaces a memset of the whole [512][n]
-       array before the launch. */
-#pragma unroll 8
-    for( int t=FD_OPS_ZBASE; t<FD_OPS_MAX; t++ ) ops[(uint64_t)t*n + i] = 0;
-  }
-#endif
   /* the two-pass recoder, S's digits parked in this lane's slots of the
      wave's SHA-512 stage (free once the digest is out) */
   typedef __attribute__((address_space(3))) uint16_t lds_u16;
@@ -259,12 +236,9 @@ FD_DEV int fd_wave_max( int x ) {
   for( int o=32; o>0; o>>=1 ) { int y = __shfl_xor( x, o, 64 ); x = y > x ? y : x; }
   return x;
 }
-/* FD_PREP2_DIRECT 1: the schedule wave fetches message bytes into
-   registers (fd_sha2_schedule_direct), so a front-end block holds only
-   the 8 KiB chunk ring */
-#ifndef FD_PREP2_DIRECT
-#define FD_PREP2_DIRECT 1
-#endif
+/* The schedule wave fetches message bytes into registers
+   (fd_sha2_schedule_direct), so a front-end block holds only the 8 KiB
+   chunk ring (an LDS-staged schedule wave was the round-4 variant). */
 #ifdef FD_FRONT_STAMPS
 /* diagnostic builds only: [0] prep round wave, [1] decomp, [2] prep
    schedule wave, [3] prep round wave up to its digest (the rest of [0] is
@@ -277,7 +251,7 @@ static __device__ __forceinline__ void
 fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz,
                fd_ed25519_gpu_desc_t const * __restrict__ desc,
                int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start, int strict,
-               fd_lds_u8 * stage, fd_sha2_lds_ring * ring, uint32_t * __restrict__ sdig, uint32_t tag ) {
+               fd_sha2_lds_ring * ring, uint32_t * __restrict__ sdig, uint32_t tag ) {
   uint32_t const wv = threadIdx.x >> 6;
   bool live = i < n;
   fd_ed25519_gpu_desc_t d = live ? desc[i] : fd_ed25519_gpu_desc_t{ 0, 0, 0, 0 };
@@ -308,12 +282,7 @@ fd_prep2_body( uint64_t i, uint64_t n, uint8_t const * __restrict__ blob, uint64
   uint32_t nblk = pend ? (uint32_t)((64ULL + sz + 17ULL + 127ULL) >> 7) : 0u;
   uint32_t nmax = (uint32_t)__builtin_amdgcn_readfirstlane( fd_wave_max( (int)nblk ) );
   if( wv ) {     /* the message / schedule wave */
-#if FD_PREP2_DIRECT
-    (void)stage;
     fd_sha2_schedule_direct( ring, pend, R, A, M, sz, nblk, nmax );
-#else
-    fd_sha2_schedule( ring, stage, pend, R, A, M, sz, nblk, nmax );
-#endif
     return;
   }
   uint64_t dig[8];
@@ -566,19 +535,10 @@ fd_k_decomp( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd
    shared SIMD's pace (111 -> 225-280 us, depth-3 trace,
    tools/lat_trace3.py).  Round 3: two-wave blocks, prep as a wave pair
    (fd_prep2_body; decomp blocks then hold 128 points). */
-/* FD_PREP2 1: prep blocks are wave pairs (fd_prep2_body: one wave runs
-   the SHA-512 rounds, its partner the message words and schedule), decomp
-   blocks two waves of points; 0: one-wave blocks, one lane per signature
-   (fd_prep_body) */
-#ifndef FD_PREP2
-#define FD_PREP2 1
-#endif
-#ifndef FD_FRONT_WAVES
-#define FD_FRONT_WAVES (FD_PREP2 ? 2 : 1)
-#endif
-#if FD_PREP2 && FD_FRONT_WAVES != 2
-#error "fd_prep2_body runs on exactly two waves per block (rounds + schedule)"
-#endif
+/* Prep blocks are wave pairs (fd_prep2_body: one wave runs the SHA-512
+   rounds, its partner the message words and schedule), decomp blocks two
+   waves of points. */
+#define FD_FRONT_WAVES 2
 /* The S pass of the recoder (fd_recode2_s) run ahead for batches of at
    most FD_SDIG_SIGS signatures, on the first decomp block's second wave,
    which holds no points then (2n <= 64): the digits go to the slot's
@@ -617,33 +577,15 @@ fd_k_front( uint64_t n, uint8_t const * __restrict__ blob, uint64_t blob_sz, fd_
             int32_t * __restrict__ status, uint8_t * __restrict__ ops, int32_t * __restrict__ op_start,
             int32_t * __restrict__ pstat, int32_t * __restrict__ pts, int portable, int strict, uint32_t nb_prep,
             uint32_t * __restrict__ sdig, uint32_t tag ) {
-#if FD_PREP2 && FD_PREP2_DIRECT
   __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
-  fd_lds_u8 * const sha_stage = NULL;
-#elif FD_PREP2
-  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_SHA_STAGE_BYTES];   /* the schedule wave's */
-  __shared__ __attribute__((aligned(16))) fd_sha2_ring sha_ring;
-#else
-  __shared__ __attribute__((aligned(16))) uint8_t sha_stage[FD_FRONT_WAVES*FD_SHA_STAGE_BYTES];
-#endif
-#ifdef FD_FRONT_PRIO
-  __builtin_amdgcn_s_setprio( FD_FRONT_PRIO );   /* experiment: issue ahead of co-resident quad-DSM waves */
-#endif
 #ifdef FD_FRONT_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if( blockIdx.x < nb_prep ) {
-#if FD_PREP2
+  if( blockIdx.x < nb_prep )
     fd_prep2_body( (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u), n, blob, blob_sz, desc, status, ops, op_start, strict,
-                   (fd_lds_u8 *)sha_stage, (fd_sha2_lds_ring *)&sha_ring, strict ? NULL : sdig, tag );
-#else
-    fd_prep_body( (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, status, ops, op_start, strict, (fd_lds_u8 *)sha_stage, NULL, 1 );
-#endif
-  }
-#if FD_PREP2
+                   (fd_sha2_lds_ring *)&sha_ring, strict ? NULL : sdig, tag );
   else if( sdig && !strict && n <= FD_SDIG_SIGS && blockIdx.x == nb_prep && threadIdx.x >= 64u )
     fd_sdig_body( (uint64_t)threadIdx.x - 64u, n, blob, blob_sz, desc, sdig, tag );   /* this wave holds no points: 2n <= 64 */
-#endif
   else
     fd_decomp_body( (uint64_t)(blockIdx.x - nb_prep) * blockDim.x + threadIdx.x, n, blob, blob_sz, desc, NULL, pstat, pts, portable, strict );
 #ifdef FD_FRONT_STAMPS
@@ -1001,22 +943,12 @@ FD_QDEV void fd_q_tab_store( int32_t * p, fe const & v ) {
   q[2] = make_int4( v.v[8], v.v[9], 0, 0 );
 }
 
-#ifndef FD_QUAD_ILP
-#define FD_QUAD_ILP 0
-#endif
-#ifndef FD_QUAD_DPP_AND
-#define FD_QUAD_DPP_AND 1
-#endif
-/* products of the latency kernel.  FD_QUAD_ILP 1 = independent column
-   chains (fd_fe_mul_ilp): measured equal (quad DSM 0.441 ms either way at
-   4,096 signatures) -- a lone wave issues about one instruction per 4-5
-   cycles whatever its ILP, so its latency follows its instruction count,
-   and the absorbed chain has fewer instructions. */
-#if FD_QUAD_ILP
-#define FD_QMUL fd_fe_mul_ilp
-#else
+/* products of the latency kernel: the absorbed column chain (fd_fe_mul).
+   Independent column chains (fd_fe_mul_ilp) measured equal (quad DSM
+   0.441 ms either way at 4,096 signatures) -- a lone wave issues about one
+   instruction per 4-5 cycles whatever its ILP, so its latency follows its
+   instruction count, and the absorbed chain has fewer instructions. */
 #define FD_QMUL fd_fe_mul
-#endif
 
 /* The lane-split DSMs' prologue reads, all issued before any is used (a
    lone wave otherwise pays one memory round trip per dependent load: the
@@ -1246,14 +1178,6 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
   if( live && q == 0u ) out[i] = code;
 }
 
-/* diagnostic builds only (FD_PREP_DYN_LDS > 0, tools/gpu.sh pmcprep):
-   extra dynamic LDS per fd_k_prep block (built with FD_PREP_WG 256) so
-   one block (4 waves) fills a CU -- one wave per SIMD instead of four -- to split the prep's wave
-   cycles into its own dependency waits and the other waves' turns */
-#ifndef FD_PREP_DYN_LDS
-#define FD_PREP_DYN_LDS 0
-#endif
-
 extern "C" __global__ void __launch_bounds__(64)
 fd_k_dsm_quad( uint64_t n, int32_t const * __restrict__ status, int32_t const * __restrict__ pstat,
                int32_t const * __restrict__ pts, uint8_t const * __restrict__ ops, int32_t const * __restrict__ op_start,
@@ -1369,13 +1293,10 @@ FD_QDEV void fd_o_carry( int64_t & s, int64_t & nx, uint32_t w, uint32_t m ) {
    crossbar without touching LDS memory.  Its latency is off the product's
    chain: the partner limbs feed only the terms with J' >= 5, issued after
    the swizzles' ~30 instructions of operand set-up and early terms.
-   FD_OCT_SWIZZLE: 0 = g's partner limbs by permlane copy/swap/select, 1 =
-   by swizzle, 2 = by swizzle, sent pre-scaled by the receiver's J' >= 5
-   factor.  Main-loop cycles per single-signature wave, 2 rounds on one
-   box: 697,845 / 685,876 / 674,928 (profiles/r04_oct_exchange_ab.jsonl). */
-#ifndef FD_OCT_SWIZZLE
-#define FD_OCT_SWIZZLE 2
-#endif
+   g's partner limbs go by swizzle, sent pre-scaled by the receiver's
+   J' >= 5 factor (against a permlane copy/swap/select and an unscaled
+   swizzle: main-loop cycles per single-signature wave 674,928 vs 697,845
+   / 685,876, profiles/r04_oct_exchange_ab.jsonl). */
 FD_QDEV int32_t fd_o_partner( int32_t x ) { return __builtin_amdgcn_ds_swizzle( x, 0x401F ); }
 
 /* out = f*g for this lane's half (h = 0: limbs 0-4, h = 1: limbs 5-9);
@@ -1384,7 +1305,6 @@ FD_QDEV int32_t fd_o_partner( int32_t x ) { return __builtin_amdgcn_ds_swizzle( 
 template<int BIASED=0>
 FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c ) {
   fd_oops o;
-#if FD_OCT_SWIZZLE == 2
   /* the partner limbs only ever enter J' >= 5 terms, always scaled by this
      lane's m19: the partner sends them scaled for us (h = 1 sends 19 g,
      h = 0 sends g), so the swizzle results feed the MACs directly */
@@ -1397,31 +1317,12 @@ FD_QDEV void fd_o_mul( fh & out, fh const & f, fh const & g, fd_octc const & c )
   }
 #pragma unroll
   for( int j=0; j<5; j++ ) fd_o_both( f.v[j], o.F[j], o.F[5+j] );
-#elif FD_OCT_SWIZZLE
-#pragma unroll
-  for( int j=0; j<5; j++ ) { o.G[j] = g.v[j]; o.G[5+j] = fd_o_partner( g.v[j] ); }
-#pragma unroll
-  for( int j=0; j<5; j++ ) fd_o_both( f.v[j], o.F[j], o.F[5+j] );
-#else
-#pragma unroll
-  for( int j=0; j<5; j++ ) {
-    fd_o_both( f.v[j], o.F[j], o.F[5+j] );
-    int32_t a, b; fd_o_both( g.v[j], a, b );
-    o.G[j] = g.v[j]; o.G[5+j] = (int32_t)fd_sel( c.hm, (uint32_t)a, (uint32_t)b );
-  }
-#endif
 #pragma unroll
   for( int i=1; i<10; i+=2 ) {
     o.FA[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sA) );
     o.FB[i] = fd_opaque( (int32_t)((uint32_t)o.F[i] << c.sB) );
   }
   o.G19[0] = 0;
-#if FD_OCT_SWIZZLE != 2
-#pragma unroll
-  for( int j=1; j<5; j++ )  o.G19[j] = fd_opaque( (int32_t)(19u   * (uint32_t)o.G[j]) );
-#pragma unroll
-  for( int j=5; j<10; j++ ) o.G19[j] = fd_opaque( (int32_t)(c.m19 * (uint32_t)o.G[j]) );
-#endif
 
   int64_t S[5];
   uint64_t const hm64 = ((uint64_t)c.hm << 32) | c.hm;
@@ -1779,16 +1680,14 @@ fd_k_dsm_setup( uint64_t n, int32_t const * __restrict__ status, int32_t const *
 
 /* D step: p1p1 -> p2 ([X,Y,Z] = [t0 t3, t1 t2, t2 t3], avx/fd_ed25519_ge.c:
    521-522), then DBL_MIX(SQN([X+Y,Y,X,Z];1,1,1,2)) (:493-498) */
-/* FD_POOL_BIASED 1 (default): the products whose limbs feed only the
+/* The products whose limbs feed only the
    lane mixes (the doubling's four squarings; an addition's X, Y and its
    four op products) hand them over with their carry biases in
    (fd_fe_limbs_t<1>: one instruction fewer per limb), and the mixes, which
    add three operands anyway, fold the biases into constants: 40 VALU
    fewer per doubling, 60 per addition.  Limbs that feed a product stay
    exact.  beta_k = 2^25 (even k) / 2^24 (odd k). */
-#ifndef FD_POOL_BIASED
 #define FD_POOL_BIASED 1
-#endif
 #define FD_BETA(k) ((k) & 1 ? (1u<<24) : (1u<<25))
 /* DBL_MIX [a-b-c, b+c, b-c, d-b+c] on biased a, b, c, d:
    t = b + c + beta (one v_add3), out0 = a - t, out1 = t - beta, out2 = b - c,
@@ -1813,15 +1712,9 @@ FD_DEV void fd_pool_dbl( fe4 & vt ) {
     fd_fe_chain3( Z, X, Y, cz, cx, cy );
   }
   fe xy; fd_fe_add( xy, X, Y );
-#if FD_POOL_BIASED
   fd_fe_sqn2<1>( vt.l[0], xy, 1, vt.l[1], Y, 1 );
   fd_fe_sqn2<1>( vt.l[2], X, 1, vt.l[3], Z, 2 );
   v_dbl_mix_b( vt );
-#else
-  fd_fe_sqn2( vt.l[0], xy, 1, vt.l[1], Y, 1 );
-  fd_fe_sqn2( vt.l[2], X, 1, vt.l[3], Z, 2 );
-  v_dbl_mix( vt );
-#endif
 }
 
 /* A step: p1p1 -> p3 ([Z,Y,X,T], :506-508) then
@@ -1843,13 +1736,9 @@ FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, uint64_t estri
   fe h0, h1, h2, h3;   /* P, Q, R, S */
   {
     fe xy, ymx;
-#if FD_POOL_BIASED
     /* X, Y biased: X + Y - 2 beta, Y - X (the biases cancel) */
 #pragma unroll
     for( int k=0; k<10; k++ ) xy.v[k] = (int32_t)((uint32_t)X.v[k] + (uint32_t)Y.v[k] - 2u*FD_BETA( k ));
-#else
-    fd_fe_add( xy, X, Y );
-#endif
     fd_fe_sub( ymx, Y, X );
     fd_fe_mul2<FD_POOL_BIASED, FD_POOL_BIASED>( h0, xy, E2, h1, Z, E0 );
     fd_fe_mul2<FD_POOL_BIASED, FD_POOL_BIASED>( h2, ymx, E1, h3, T, E3 );
@@ -1858,18 +1747,12 @@ FD_DEV void fd_pool_add( fe4 & vt, int op, int32_t const * tab_i, uint64_t estri
 #pragma unroll
   for( int k=0; k<10; k++ ) {
     uint32_t P = h0.v[k], Q = h1.v[k], R = h2.v[k], S = h3.v[k];
-#if FD_POOL_BIASED
     /* biased P, Q, R, S: P - R, P + R - 2 beta; Q2' = 2Q - beta (one
        v_lshl_add), o2 = Q2' - S, o3 = Q2' + S - 2 beta */
     uint32_t const bt = FD_BETA( k );
     uint32_t Q2 = 2u*Q - bt, o2 = Q2 - S, o3 = Q2 + S - 2u*bt;
     vt.l[0].v[k] = (int32_t)(P - R);
     vt.l[1].v[k] = (int32_t)(P + R - 2u*bt);
-#else
-    uint32_t Q2 = 2u*Q, o2 = Q2 - S, o3 = Q2 + S;
-    vt.l[0].v[k] = (int32_t)(P - R);
-    vt.l[1].v[k] = (int32_t)(P + R);
-#endif
     vt.l[2].v[k] = (int32_t)fd_sel( mp, o3, o2 );
     vt.l[3].v[k] = (int32_t)fd_sel( mp, o2, o3 );
   }
@@ -1885,9 +1768,6 @@ FD_DEV void fd_mem_fence( void ) { asm volatile( "" ::: "memory" ); }
    128 slots x 8 B = 20 KiB per wave, 8 waves = the CU's 160 KiB).  Slot s holds signature
    gw + s*nwaves. */
 #define FD_POOL 128
-#ifndef FD_POOL_PRIO
-#define FD_POOL_PRIO 0
-#endif
 struct fd_pool_lds { uint64_t st[20][FD_POOL]; };   /* limb pairs: 8-byte LDS accesses (64 banks) */
 
 #ifdef FD_POOL_STAMPS
@@ -1966,9 +1846,6 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
 #ifdef FD_POOL_STAMPS
     unsigned long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-#if FD_POOL_PRIO
-    __builtin_amdgcn_s_setprio( 2 );          /* bookkeeping: issue ahead of the other wave's step math */
-#endif
     int m0 = mt[0], m1 = mt[1];
     int t0 = m0 >> 8, t1 = m1 >> 8;
     int l0 = t0 < FD_OPS_MAX, l1 = t1 < FD_OPS_MAX;
@@ -2038,9 +1915,6 @@ fd_k_dsm_pool( uint64_t n, int32_t const * __restrict__ status, int32_t const * 
     uint32_t s = act ? ((uint32_t)pm >> 24) & 127u : lane;
     int mm = pm & 0xffffff;
     int nm = mm;
-#if FD_POOL_PRIO
-    __builtin_amdgcn_s_setprio( 0 );
-#endif
 #ifdef FD_POOL_STAMPS
     unsigned long pt1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2301,15 +2175,15 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
   int quad = n < pool_min && !portable && (n <= quad_max || n <= oct_max);
   /* op streams are zeroed by their own prep lanes (only rows of
      signatures still pending after the S check are ever read); the
-     FD_PREP_ZERO 0 build memsets the step-major array first */
-  if( !quad && !FD_PREP_ZERO ) {
+     step-major array is memset first */
+  if( !quad ) {
     hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
     if( e != hipSuccess ) return e;
   }
   if( quad ) {
     /* latency path: prep and decomp in one launch (their time lands in phase 1) */
     unsigned const bt = 64u*FD_FRONT_WAVES;
-    unsigned const ps = FD_PREP2 ? 64u : bt;   /* signatures per prep block */
+    unsigned const ps = 64u;                   /* signatures per prep block (a wave pair) */
     unsigned const fp = (unsigned)((n + ps - 1) / ps), fd = (unsigned)(((portable ? n : 2*n) + bt - 1) / bt);
     /* the tag that publishes this launch's S digits (fd_sdig_body): never 0
        (the scratch starts zeroed), never an earlier launch's on this buffer */
@@ -2320,7 +2194,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_front( uint64_t n, uint8_t const * b
                         w->pstat, w->pts, portable, strict, fp, w->sdig, tag );
     if( ev ) hipEventRecord( ev[1], stream );
   } else {
-    hipLaunchKernelGGL( fd_k_prep,   dim3((unsigned)((n + FD_PREP_WG - 1) / FD_PREP_WG)), dim3(FD_PREP_WG), FD_PREP_DYN_LDS, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
+    hipLaunchKernelGGL( fd_k_prep,   dim3((unsigned)((n + FD_PREP_WG - 1) / FD_PREP_WG)), dim3(FD_PREP_WG), 0, stream, n, blob, blob_sz, desc, w->status, w->ops, w->op_start, strict,
                         (uint64_t *)NULL );
     if( ev ) hipEventRecord( ev[1], stream );
     hipLaunchKernelGGL( fd_k_decomp, dim3(nb2), dim3(256), 0, stream, n, blob, blob_sz, desc, w->status, w->pstat, w->pts, portable, strict );
@@ -2395,7 +2269,7 @@ extern "C" hipError_t fd_ed25519_gpu_launch_prep_k( uint64_t n, uint8_t const * 
                                                    fd_ed25519_gpu_desc_t const * desc, fd_ed25519_gpu_work_t const * w,
                                                    uint64_t * kout, hipStream_t stream ) {
   if( !n ) return hipSuccess;
-  if( !FD_PREP_ZERO ) {
+  {
     hipError_t e = hipMemsetAsync( w->ops, 0, (size_t)FD_OPS_MAX * n, stream );
     if( e != hipSuccess ) return e;
   }

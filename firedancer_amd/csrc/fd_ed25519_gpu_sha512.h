@@ -62,18 +62,12 @@ FD_DEV uint64_t fd_ld_u64_unaligned( uint8_t const * p ) {
   return ((uint64_t)__builtin_amdgcn_alignbit( w2, w1, mis * 8u ) << 32) | __builtin_amdgcn_alignbit( w1, w0, mis * 8u );
 }
 
-#ifndef FD_SHA_BARRIER
-#define FD_SHA_BARRIER 1
-#endif
 FD_DEV uint64_t fd_opaque64u( uint64_t x ) {
-#if defined(__HIP_DEVICE_COMPILE__) && FD_SHA_BARRIER
+#if defined(__HIP_DEVICE_COMPILE__)
   asm( "" : "+v"(x) );
 #endif
   return x;
 }
-#ifndef FD_SHA_B3
-#define FD_SHA_B3 1
-#endif
 /* 3-input bitwise ops as one v_bitop3_b32 per 32-bit half (gfx950):
    truth tables 0x96 (x^y^z) and 0xE8 (majority), both symmetric in their
    inputs, so independent of the operand-order convention. */
@@ -105,31 +99,21 @@ FD_DEV uint32_t fd_bitop3_ca( uint32_t x, uint32_t y, uint32_t z ) {
 #endif
 }
 FD_DEV uint64_t fd_ch64( uint64_t e, uint64_t f, uint64_t g ) {
-  if( !FD_SHA_B3 ) return (e&f) ^ (~e&g);
   return fd_opaque64u( ((uint64_t)fd_bitop3_ca( (uint32_t)(e>>32), (uint32_t)(f>>32), (uint32_t)(g>>32) ) << 32)
                        | fd_bitop3_ca( (uint32_t)e, (uint32_t)f, (uint32_t)g ) );
 }
 FD_DEV uint64_t fd_xor3_64( uint64_t x, uint64_t y, uint64_t z ) {
-  if( !FD_SHA_B3 ) return x ^ y ^ z;
   return fd_opaque64u( ((uint64_t)fd_bitop3_96( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
                        | fd_bitop3_96( (uint32_t)x, (uint32_t)y, (uint32_t)z ) );
 }
 FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
-  if( !FD_SHA_B3 ) return (x&y) ^ (x&z) ^ (y&z);
   return fd_opaque64u( ((uint64_t)fd_bitop3_e8( (uint32_t)(x>>32), (uint32_t)(y>>32), (uint32_t)(z>>32) ) << 32)
                        | fd_bitop3_e8( (uint32_t)x, (uint32_t)y, (uint32_t)z ) );
 }
 
-#ifndef FD_SHA_ASSOC
-#define FD_SHA_ASSOC 1
-#endif
-#ifndef FD_SHA_UNROLL
-#define FD_SHA_UNROLL 0
-#endif
 /* The adds are grouped so the chain from e (and a) to the next round is
    short: h + K + W does not depend on this round's e, S0 + maj is formed
    beside T1; the barriers keep LLVM from re-linearizing the sums. */
-#if FD_SHA_ASSOC
 #define FD_SHA_ROUND(j,kt) do {                                                   \
     uint64_t hkw = fd_opaque64u( h + (kt) + w[j] );                             \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
@@ -140,16 +124,6 @@ FD_DEV uint64_t fd_maj64( uint64_t x, uint64_t y, uint64_t z ) {
     uint64_t t2 = fd_opaque64u( S0 + mj );                                      \
     h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+t2;                              \
   } while(0)
-#else
-#define FD_SHA_ROUND(j,kt) do {                                                   \
-    uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
-    uint64_t ch = fd_ch64( e, f, g );                                             \
-    uint64_t t1 = h + S1 + ch + (kt) + w[j];                                    \
-    uint64_t S0 = fd_xor3_64( fd_rotr64(a,28), fd_rotr64(a,34), fd_rotr64(a,39) ); \
-    uint64_t mj = fd_maj64( a, b, c );                                          \
-    h=g; g=f; f=e; e=d+t1; d=c; c=b; b=a; a=t1+S0+mj;                           \
-  } while(0)
-#endif
 
 /* 80 rounds as 16 + 4 x 16 so every index into the 16-word schedule
    ring is a compile-time constant (no dynamic register indexing). */
@@ -157,11 +131,7 @@ FD_DEV void fd_sha512_compress( uint64_t (&st)[8], uint64_t (&w)[16] ) {
   uint64_t a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
 #pragma unroll
   for( int j=0; j<16; j++ ) FD_SHA_ROUND( j, fd_gpu_sha512_k[j] );
-#if FD_SHA_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
   for( int r=16; r<80; r+=16 ) {
 #pragma unroll
     for( int j=0; j<16; j++ ) {
@@ -305,7 +275,7 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
 
    One wave of a two-wave workgroup runs the 80 rounds of every block; its
    partner forms the message words (fetched into registers a block ahead,
-   fd_sha2_schedule_direct below; fd_sha2_schedule stages them through LDS
+   fd_sha2_schedule_direct below; an LDS-staged variant was round 4's
    as above, the FD_PREP2_DIRECT 0 build) and the
    message schedule W[16..79] and hands them over through an LDS ring of
    two 8-word chunks, synchronised by workgroup barriers:
@@ -326,17 +296,9 @@ FD_DEV void fd_sha512_blocks( uint64_t (&st)[8], uint8_t const * R, uint8_t cons
 struct fd_sha2_ring { uint64_t w[2][FD_SHA2_CW][64]; };   /* 8 KiB, lane-contiguous (no bank conflicts) */
 typedef __attribute__((address_space(3))) fd_sha2_ring fd_sha2_lds_ring;
 
-/* FD_SHA2_WK 1: the schedule wave hands over W[t] + K[t] (the constant is
-   an immediate there, its loop being unrolled); the round wave then has no
-   scalar load of the chunk's constants -- and no wait on it after every
-   barrier -- and one 64-bit add less per round (276 -> 264 instructions
-   per 8-round chunk).  Measured on one signature (tools/oct_clock.py,
-   profiles/r05_sha2_wk_ab.jsonl): call p50 0.3565 ms (0) vs 0.3582 (1) --
-   the schedule wave, one add more per word, paces the pair as much as the
-   round wave does -- so 0, W[t] only, stays the default. */
-#ifndef FD_SHA2_WK
-#define FD_SHA2_WK 0
-#endif
+/* The schedule wave hands over W[t] alone; handing over W[t] + K[t]
+   (no scalar constant load in the round wave) measured no faster: call
+   p50 0.3565 ms vs 0.3582 (profiles/r05_sha2_wk_ab.jsonl). */
 #define FD_SHA_ROUND_W(wj,kt) do {                                                 \
     uint64_t hkw = fd_opaque64u( h + (kt) + (wj) );                             \
     uint64_t S1 = fd_xor3_64( fd_rotr64(e,14), fd_rotr64(e,18), fd_rotr64(e,41) ); \
@@ -362,13 +324,8 @@ FD_DEV void fd_sha2_rounds( uint64_t (&st)[8], fd_sha2_lds_ring * ring, uint32_t
       uint64_t W[FD_SHA2_CW];
 #pragma unroll
       for( int j=0; j<FD_SHA2_CW; j++ ) W[j] = ring->w[k & 1u][j][lane];
-#if FD_SHA2_WK
-#pragma unroll
-      for( int j=0; j<FD_SHA2_CW; j++ ) FD_SHA_ROUND_W( W[j], 0ULL );
-#else
 #pragma unroll
       for( int j=0; j<FD_SHA2_CW; j++ ) FD_SHA_ROUND_W( W[j], fd_gpu_sha512_k[FD_SHA2_CW*ch + j] );
-#endif
       k++;
     }
     bool upd = blk < nblk;
@@ -377,63 +334,6 @@ FD_DEV void fd_sha2_rounds( uint64_t (&st)[8], fd_sha2_lds_ring * ring, uint32_t
   }
 }
 
-/* the partner wave: message words of R || A || M(sz) (PRE = 64) and the
-   schedule, chunk by chunk into the ring; live lanes only stage and read
-   message bytes (stage: this wave's FD_SHA_STAGE_BYTES of LDS) */
-FD_DEV void fd_sha2_schedule( fd_sha2_lds_ring * ring, fd_lds_u8 * stage, bool live, uint8_t const * R, uint8_t const * A,
-                              uint8_t const * M, uint32_t sz, uint32_t nblk, uint32_t nblk_max ) {
-  uint32_t const lane = threadIdx.x & 63u;
-  uint64_t L = 64ULL + sz;
-  uint8_t const * end = M + sz;
-  uint64_t w[16];
-  uint32_t dw[33];
-#pragma unroll
-  for( int i=0; i<16; i++ ) w[i] = 0ULL;
-  uint32_t k = 0;
-  if( live ) fd_sha_stage( stage, fd_floor16( M ), end );
-  for( uint32_t blk=0; blk<nblk_max; blk++ ) {
-    bool on = live && blk < nblk;
-    if( blk == 0u ) {
-      if( live ) {
-#pragma unroll
-        for( int i=0; i<4; i++ ) w[i]   = fd_bswap64( fd_ld_u64_unaligned( R + 8*i ) );
-#pragma unroll
-        for( int i=0; i<4; i++ ) w[4+i] = fd_bswap64( fd_ld_u64_unaligned( A + 8*i ) );
-      }
-      uint32_t d = (uint32_t)((uintptr_t)M & 15u);
-      fd_sha_read( dw, stage, d );
-      fd_sha_words<8, 64>( w, dw, (d & 3u) * 8u, -64, sz, L, nblk == 1u );
-      fd_sha_next( w, stage, fd_floor16( M + 64 ), end, live && nblk > 1u );
-    } else {
-      /* the block index as a VGPR value: with the wave-uniform (SGPR) loop
-         counter LLVM (ROCm 7.2) selects a scalar operand where a vector one
-         is required in the staging address math and fails with "Operand has
-         incorrect register class" */
-      uint32_t const bv = (uint32_t)fd_opaque( (int32_t)blk );
-      int64_t mbase = (int64_t)bv*128 - 64;
-      uint32_t d = (uint32_t)(((uintptr_t)M + (uintptr_t)mbase) & 15u);
-      fd_sha_read( dw, stage, d );
-      fd_sha_words<0, 64>( w, dw, (d & 3u) * 8u, mbase, sz, L, bv == nblk-1u );
-      fd_sha_next( w, stage, fd_floor16( M + mbase + 128 ), end, on && bv + 1u < nblk );
-    }
-#pragma unroll
-    for( int ch=0; ch<FD_SHA2_CHUNKS; ch++ ) {
-#pragma unroll
-      for( int j=0; j<FD_SHA2_CW; j++ ) {
-        int const t = FD_SHA2_CW*ch + j;
-        if( t >= 16 ) {
-          uint64_t w15 = w[(t+1)&15], w2 = w[(t+14)&15];
-          uint64_t s0 = fd_xor3_64( fd_rotr64(w15,1), fd_rotr64(w15,8), fd_shr64(w15,7) );
-          uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
-          w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
-        }
-        ring->w[k & 1u][j][lane] = FD_SHA2_WK ? w[t&15] + fd_gpu_sha512_k[t] : w[t&15];
-      }
-      __syncthreads();
-      k++;
-    }
-  }
-}
 
 /* The partner wave without LDS staging: each block's 144-byte window is
    fetched straight into registers (9 x 16-byte loads from the dword
@@ -496,7 +396,7 @@ FD_DEV void fd_sha2_schedule_direct( fd_sha2_lds_ring * ring, bool live, uint8_t
           uint64_t s1 = fd_xor3_64( fd_rotr64(w2,19), fd_rotr64(w2,61), fd_shr64(w2,6) );
           w[t&15] = w[t&15] + s0 + w[(t+9)&15] + s1;
         }
-        ring->w[k & 1u][j][lane] = FD_SHA2_WK ? w[t&15] + fd_gpu_sha512_k[t] : w[t&15];
+        ring->w[k & 1u][j][lane] = w[t&15];
       }
       __syncthreads();
       k++;
