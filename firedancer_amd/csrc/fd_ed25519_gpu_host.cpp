@@ -579,7 +579,12 @@ extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) {
 static void fd_reclaim_orphans( fd_ed25519_gpu_t * g ) {
   for( int s=0; s<g->depth; s++ ) {
     fd_ed25519_gpu_slot * sl = &g->slot[s];
-    if( (sl->orphan || sl->retiring) && hipEventQuery( sl->done ) == hipSuccess ) { sl->orphan = 0; sl->retiring = 0; sl->ticket = 0; sl->staged = 0; }
+    if( (sl->orphan || sl->retiring) && hipEventQuery( sl->done ) == hipSuccess ) {
+      /* an orphan is nobody's: its stage (if the failing caller has not
+         unstaged it yet) goes with it; a retiring slot keeps its owner's */
+      if( sl->orphan ) sl->staged = 0;
+      sl->orphan = 0; sl->retiring = 0; sl->ticket = 0;
+    }
   }
 }
 
@@ -596,10 +601,15 @@ static void fd_abandon_ticket( fd_ed25519_gpu_t * g, unsigned long ticket ) {
    reclaim it, so a caller that submits right after such a poll finds the
    slot as it would have without the early return.  Caller holds g->lock.
    Returns 1 if a slot came back. */
+/* the bound on that wait under the lock: a retiring slot's event follows
+   its codes within microseconds; one that has not fired by then (a wedged
+   device) is left for later rather than stalling every engine caller for
+   the whole engine timeout */
+#define FD_RETIRE_WAIT_NS 200000L
 static int fd_wait_retiring( fd_ed25519_gpu_t * g ) {
   for( int s=0; s<g->depth; s++ )
     if( g->slot[s].retiring ) {
-      if( fd_event_wait( g->slot[s].done, fd_timeout( g ) ) ) return 0;
+      if( fd_wait_query( fd_event_query, (void *)g->slot[s].done, FD_RETIRE_WAIT_NS, FD_RETIRE_WAIT_NS ) != 1 ) return 0;
       fd_reclaim_orphans( g );
       return 1;
     }
@@ -624,7 +634,12 @@ extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25
 extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
   if( !g ) return;
   std::lock_guard<std::mutex> guard( g->lock );
-  for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) g->slot[s].staged = 0;
+  /* only a slot still lent out and idle: a failed submit may have
+     orphaned it meanwhile, and once reclaimed and lent to another caller
+     that caller's stage must not be cleared by this late unstage
+      */
+  for( int s=0; s<g->depth; s++ )
+    if( g->slot[s].h_blob == blob && !g->slot[s].ticket && !g->slot[s].orphan ) g->slot[s].staged = 0;
 }
 
 /* a free slot: the staged one owning `blob` if any, else any unstaged one

@@ -27,6 +27,7 @@
 
 #include <string.h>
 #include <time.h>
+#include <mutex>
 #include <vector>
 #include "fd_ed25519_gpu.h"
 #include "fd_ed25519_gpu_desc.h"
@@ -40,6 +41,8 @@ struct fd_ed25519_gpu_multi {
   long                                   timeout_ns;   /* bound on one multi call (< 0: none) */
   unsigned long                          dealt[64];    /* signatures each engine ran in the last call */
   double                                 nsps[64];     /* each engine's measured ns per signature (EMA; 0: unknown) */
+  std::mutex                             call;         /* calls on one handle run one at a time (dealt / nsps are
+                                                          per-handle state); each saturates every engine */
 };
 
 /* the guided chunks' floor: 65,536 signatures (a launch that still fills
@@ -104,7 +107,9 @@ FD_EXPORT int fd_ed25519_gpu_multi_set_timeout( fd_ed25519_gpu_multi_t * m, long
   return 0;
 }
 FD_EXPORT unsigned long fd_ed25519_gpu_multi_dealt( fd_ed25519_gpu_multi_t const * m, int i ) {
-  return ( m && i >= 0 && i < (int)m->eng.size() ) ? m->dealt[i] : 0UL;
+  if( !m || i < 0 || i >= (int)m->eng.size() ) return 0UL;
+  std::lock_guard<std::mutex> guard( const_cast<fd_ed25519_gpu_multi_t *>( m )->call );
+  return m->dealt[i];
 }
 
 /* cut descs [0,n) into guided chunks (remaining / (2 nd), clamped to
@@ -131,6 +136,7 @@ FD_EXPORT int fd_ed25519_gpu_multi_verify_packed( fd_ed25519_gpu_multi_t * m, un
                                                   unsigned long blob_sz, fd_ed25519_gpu_desc_t const * desc, int * out ) {
   if( !m || (n && (!desc || !out)) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
+  std::lock_guard<std::mutex> guard( m->call );
   int nd = (int)m->eng.size();
   /* every chunk first (an ERR_ARG writes nothing); chunks fit every engine */
   unsigned long max_sigs = ~0UL, max_blob = ~0UL;
