@@ -1138,15 +1138,15 @@ FD_QDEV void fd_quad_body( uint64_t n, int32_t const * __restrict__ status, int3
     for( int k=0; k<10; k++ ) {
       int const cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;
       int const kc  = !(k & 1) ? FD_Q3_KE : (k == 1 || k == 5) ? FD_Q3_KX : FD_Q3_KO;
-      uint32_t const mP = (uint32_t)fd_opaque( D[FD_Q3_MPE + cls] ), mQ = (uint32_t)fd_opaque( D[FD_Q3_MQE + cls] );
+      uint32_t const m3 = (uint32_t)fd_opaque( D[FD_Q3_M3E + cls] );
       uint32_t const mR = (uint32_t)fd_opaque( D[FD_Q3_MRE + cls] ), mS = (uint32_t)fd_opaque( D[FD_Q3_MSE + cls] );
-      uint32_t a = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,1,1)>( hr.v[k] ) & mP) );
-      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(2,2,2,2)>( hr.v[k] ) & mQ) );
+      /* P (lanes 0, 1) or Q (lanes 2, 3): one read for both (fd_q3_entry) */
+      uint32_t b = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(1,1,2,2)>( hr.v[k] ) & m3) );
       uint32_t c = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(3,3,3,3)>( hr.v[k] ) & mR) );
       uint32_t d = (uint32_t)fd_opaque( (int32_t)((uint32_t)fd_qperm<FD_QP(0,0,0,0)>( hr.v[k] ) & mS) );
-      /* (c ^ sR) + K, (d ^ sS) + a as v_xad_u32; + (b << qs) as v_lshl_add */
-      uint32_t const x1 = fd_xad( c, sR, (uint32_t)D[kc] ), x2 = fd_xad( d, sS, a );
-      vt.v[k] = (int32_t)((b << qs) + x1 + x2);
+      /* ((d ^ sS) + ((c ^ sR) + K)) as two v_xad_u32; + (b << qs) as v_lshl_add */
+      uint32_t const x1 = fd_xad( c, sR, (uint32_t)D[kc] ), x2 = fd_xad( d, sS, x1 );
+      vt.v[k] = (int32_t)((b << qs) + x2);
     }
   }
 

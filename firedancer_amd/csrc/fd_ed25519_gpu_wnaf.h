@@ -100,33 +100,37 @@ FD_DEV uint32_t fd_q2_kind_bits( uint32_t q, int add, int neg ) {
    (25 bits: class O) fold into the operand and output masks, limbs 1 and 5
    (class X: 26-bit mask, bias 2^24 + FD_FE_RAW_X) too, and each class's
    bias into kf / K.  Signs (sA, sR, sS) stay full masks; gs, qs are shift
-   counts; IDX is the table entry lane's offset in int32s. */
+   counts; IDX is the table entry lane's offset in int32s.
+   The mix reads three source lanes, not four (round 6): no lane ever takes
+   both P and Q (D: P on q0, Q on q3; A: P on q0, q1, Q on q2, q3), so the
+   P / Q term is one read, quad_perm(1,1,2,2) -- lane 1 (P) for q0, q1,
+   lane 2 (Q) for q2, q3 -- under one mask M3 = mP | mQ, shifted by qs = 1
+   only where it carries Q on an add (P is never doubled).  The same sum,
+   term for term: 8 -> 6 instructions per limb. */
 #define FD_Q3_MAE   0
 #define FD_Q3_MAO   1
 #define FD_Q3_MBE   2
 #define FD_Q3_MBO   3
-#define FD_Q3_MPE   4
-#define FD_Q3_MPO   5
-#define FD_Q3_MQE   6
-#define FD_Q3_MQO   7
-#define FD_Q3_MRE   8
-#define FD_Q3_MRO   9
-#define FD_Q3_MSE   10
-#define FD_Q3_MSO   11
-#define FD_Q3_SA    12
-#define FD_Q3_SR    13
-#define FD_Q3_SS    14
-#define FD_Q3_GS    15
-#define FD_Q3_QS    16
-#define FD_Q3_MADD  17
-#define FD_Q3_KFE   18
-#define FD_Q3_KFO   19
-#define FD_Q3_KFX   20
-#define FD_Q3_KE    21
-#define FD_Q3_KO    22
-#define FD_Q3_KX    23
-#define FD_Q3_IDX   24
-#define FD_Q3_DW    28          /* 7 x 16 bytes */
+#define FD_Q3_M3E   4
+#define FD_Q3_M3O   5
+#define FD_Q3_MRE   6
+#define FD_Q3_MRO   7
+#define FD_Q3_MSE   8
+#define FD_Q3_MSO   9
+#define FD_Q3_SA    10
+#define FD_Q3_SR    11
+#define FD_Q3_SS    12
+#define FD_Q3_GS    13
+#define FD_Q3_QS    14
+#define FD_Q3_MADD  15
+#define FD_Q3_KFE   16
+#define FD_Q3_KFO   17
+#define FD_Q3_KFX   18
+#define FD_Q3_KE    19
+#define FD_Q3_KO    20
+#define FD_Q3_KX    21
+#define FD_Q3_IDX   22
+#define FD_Q3_DW    24          /* 6 x 16 bytes */
 FD_DEV uint32_t fd_q3_entry( uint32_t q, int kind, int dw ) {
   uint32_t w = fd_q2_kind_bits( q, kind != 0, kind == 2 );
   uint32_t const mE = (1u<<26)-1u, mO = (1u<<25)-1u;
@@ -138,15 +142,15 @@ FD_DEV uint32_t fd_q3_entry( uint32_t q, int kind, int dw ) {
   switch( dw ) {
     case FD_Q3_MAE: return m( FD_Q2_MA ) & mE;   case FD_Q3_MAO: return m( FD_Q2_MA ) & mO;
     case FD_Q3_MBE: return m( FD_Q2_MB ) & mE;   case FD_Q3_MBO: return m( FD_Q2_MB ) & mO;
-    case FD_Q3_MPE: return m( FD_Q2_MP ) & mE;   case FD_Q3_MPO: return m( FD_Q2_MP ) & mO;
-    case FD_Q3_MQE: return m( FD_Q2_MQ ) & mE;   case FD_Q3_MQO: return m( FD_Q2_MQ ) & mO;
+    case FD_Q3_M3E: return ( m( FD_Q2_MP ) | m( FD_Q2_MQ ) ) & mE;
+    case FD_Q3_M3O: return ( m( FD_Q2_MP ) | m( FD_Q2_MQ ) ) & mO;
     case FD_Q3_MRE: return m( FD_Q2_MR ) & mE;   case FD_Q3_MRO: return m( FD_Q2_MR ) & mO;
     case FD_Q3_MSE: return m( FD_Q2_MS ) & mE;   case FD_Q3_MSO: return m( FD_Q2_MS ) & mO;
     case FD_Q3_SA:  return m( FD_Q2_SA );
     case FD_Q3_SR:  return m( FD_Q2_SR );
     case FD_Q3_SS:  return m( FD_Q2_SS );
     case FD_Q3_GS:  return (w >> FD_Q2_GS) & 1u;
-    case FD_Q3_QS:  return kind ? 1u : 0u;
+    case FD_Q3_QS:  return ( kind && q >= 2u ) ? 1u : 0u;   /* Q doubled on an add (lanes 2, 3 carry Q there) */
     case FD_Q3_MADD:return kind ? ~0u : 0u;
     case FD_Q3_KFE: return sa1 - (uint32_t)nf * bE;
     case FD_Q3_KFO: return sa1 - (uint32_t)nf * bO;

@@ -749,8 +749,11 @@ static int fd_verify_tile_rx_( fd_verify_tile_t * t, void const * frag, unsigned
       FD_VT_STAMP( s4 ); FD_VT_ACC( 3, s3, s4 );
       if( oc ) {
         /* the copy is not committed yet (b->used unchanged): an overrun
-           frag or a duplicate leaves the batch as it was */
-        _mm_sfence();
+           frag or a duplicate leaves the batch as it was.  The copy's
+           loads precede the callback's seq load (x86 keeps loads in
+           order; the callback's acquire fence keeps the compiler from
+           sinking them); its streaming stores need no fence here (fd_vt_submit
+           fences before the device is told) */
         if( t->ovrn( t->octx, seq ) ) { t->diag[ FD_VERIFY_TILE_DIAG_OVRN_CNT ]++; return 0; }
         if( fd_vt_tcache_insert( t->tc, tag ) ) {
           t->diag[ FD_VERIFY_TILE_DIAG_HA_FILT_CNT ]++;

@@ -183,9 +183,10 @@ int h_quad_dsm( int32_t * out, int32_t const * A, uint8_t const * ops, int start
       for( int k=0; k<10; k++ ) {
         int cls = ( (k & 1) && k != 1 && k != 5 ) ? 1 : 0;
         int kc  = !(k & 1) ? FD_Q3_KE : (k == 1 || k == 5) ? FD_Q3_KX : FD_Q3_KO;
-        uint32_t a = (uint32_t)hr[1].v[k] & d[FD_Q3_MPE + cls], b = (uint32_t)hr[2].v[k] & d[FD_Q3_MQE + cls];
+        /* the P / Q term from one source lane: P (lane 1) for q0, q1, Q (lane 2) for q2, q3 */
+        uint32_t b = (uint32_t)hr[q < 2 ? 1 : 2].v[k] & d[FD_Q3_M3E + cls];
         uint32_t c = (uint32_t)hr[3].v[k] & d[FD_Q3_MRE + cls], e = (uint32_t)hr[0].v[k] & d[FD_Q3_MSE + cls];
-        vt[q].v[k] = (int32_t)((b << d[FD_Q3_QS]) + ((c ^ d[FD_Q3_SR]) + d[kc]) + ((e ^ d[FD_Q3_SS]) + a));
+        vt[q].v[k] = (int32_t)((b << d[FD_Q3_QS]) + ((e ^ d[FD_Q3_SS]) + ((c ^ d[FD_Q3_SR]) + d[kc])));
       }
     }
   }

@@ -66,10 +66,12 @@ struct alignas(64) line_t {
 };
 
 struct live {
-  /* corpus */
-  std::vector<std::vector<unsigned char>> frag;
-  std::vector<unsigned char>               expect;     /* per corpus entry: 1 the reference publishes it, 0 not; empty: unchecked */
-  unsigned long                            n;
+  /* corpus (shared by the tiles) */
+  std::vector<std::vector<unsigned char>> const * fragp;
+  std::vector<unsigned char> const *               expectp;   /* per corpus entry: 1 the reference publishes it, 0 not; empty: unchecked */
+  unsigned long                                    n;
+  std::vector<std::vector<unsigned char>> const & frag( void ) const { return *fragp; }
+  std::vector<unsigned char> const &               expect( void ) const { return *expectp; }
   /* link */
   line_t *        mc;
   unsigned long   depth, mask;
@@ -91,6 +93,7 @@ struct live {
   unsigned char * out; unsigned long out_sz, out_w;
   unsigned long   pub, pub_sz, mismatch, false_pub, order_err, last_seq, any_pub;
   unsigned long   warm;                 /* frags before this seq are left out of the latency stats */
+  unsigned long   pf;                   /* the input adapter prefetches frag want + pf */
   fd_verify_tile_lat_t * lat;
   FILE *          pubout;
 };
@@ -121,7 +124,7 @@ static void producer( live * L ) {
         __builtin_ia32_pause();
       }
     }
-    std::vector<unsigned char> const & f = L->frag[ s % L->n ];
+    std::vector<unsigned char> const & f = L->frag()[ s % L->n ];
     unsigned long sz = f.size();
     if( w + sz > L->dc_sz ) w = 0;
     line_t * ln = &L->mc[ s & L->mask ];
@@ -162,7 +165,19 @@ static int in_seq( void * ctx, void const ** frag, unsigned long * sz, unsigned 
     return 0;
   }
   *frag = L->dc + o; *sz = z; *ctl = c; *tsorig = t; *seq = L->want;
-  if( !L->expect.empty() && L->expect[ L->want % L->n ] ) L->taken_pass_expected++;
+  /* the input adapter prefetches the next frags the producer has already
+     published (their lines and bytes were written by another core): the
+     tile's reads of a frag then hit this core's caches, as the
+     reference's tiles keep their inputs in cache */
+  unsigned long const pf = L->pf;
+  for( unsigned long j=pf; j<=pf; j++ ) {
+    line_t const * nl = &L->mc[ (L->want + j) & L->mask ];
+    if( nl->seq.load( std::memory_order_acquire ) != L->want + j ) break;
+    unsigned char const * p = L->dc + nl->off;
+    for( unsigned long b=0; b<nl->sz; b+=64UL ) __builtin_prefetch( p + b, 0, 3 );
+  }
+  __builtin_prefetch( &L->mc[ (L->want + pf + 1UL) & L->mask ], 0, 3 );
+  if( !L->expect().empty() && L->expect()[ L->want % L->n ] ) L->taken_pass_expected++;
   L->want++; L->taken++;
   L->want_a.store( L->want, std::memory_order_relaxed );
   L->taken_a.store( L->taken, std::memory_order_relaxed );
@@ -187,9 +202,9 @@ static void publish( void * ctx, unsigned long sig, void const * frag, unsigned 
                      unsigned long tsorig, unsigned long tspub ) {
   live * L = (live *)ctx;
   unsigned long seq = ctl;
-  std::vector<unsigned char> const & f = L->frag[ seq % L->n ];
+  std::vector<unsigned char> const & f = L->frag()[ seq % L->n ];
   if( sz != f.size() || memcmp( frag, f.data(), sz ) ) L->mismatch++;
-  if( !L->expect.empty() && !L->expect[ seq % L->n ] ) L->false_pub++;
+  if( !L->expect().empty() && !L->expect()[ seq % L->n ] ) L->false_pub++;
   if( L->any_pub && seq <= L->last_seq ) L->order_err++;
   L->last_seq = seq; L->any_pub = 1;
   L->pub++; L->pub_sz += sz;
@@ -233,143 +248,185 @@ static char const * arg( int argc, char ** argv, char const * key, char const * 
   return dflt;
 }
 
+/* one tile: its link, producer, task and cnc */
+struct tile_run {
+  live                  L;
+  fd_verify_tile_cnc_t  cnc;
+  fd_verify_tile_args_t a;
+  int                   cpu_p, cpu_t;
+};
+
+static void pin( int cpu ) {
+  if( cpu < 0 ) return;
+  cpu_set_t m; CPU_ZERO( &m ); CPU_SET( cpu, &m ); sched_setaffinity( 0, sizeof(m), &m );
+}
+
 int main( int argc, char ** argv ) {
   if( argc < 2 ) { fprintf( stderr, "usage: vt_live FRAGS key=value...\n" ); return 2; }
-  static live L;
+  static std::vector<std::vector<unsigned char>> corpus;
+  static std::vector<unsigned char>               expect;
   FILE * fp = fopen( argv[1], "rb" );
   if( !fp ) { perror( argv[1] ); return 2; }
   unsigned n = 0;
   if( fread( &n, 4, 1, fp ) != 1 || !n ) return 2;
-  L.frag.resize( n );
-  unsigned long fmax = 0, sigs_total = 0;
+  corpus.resize( n );
+  unsigned long fmax = 0;
   for( unsigned i=0; i<n; i++ ) {
     unsigned s; if( fread( &s, 4, 1, fp ) != 1 ) return 2;
-    L.frag[i].resize( s );
-    if( s && fread( L.frag[i].data(), 1, s, fp ) != s ) return 2;
+    corpus[i].resize( s );
+    if( s && fread( corpus[i].data(), 1, s, fp ) != s ) return 2;
     if( s > fmax ) fmax = s;
   }
   fclose( fp );
-  L.n = n;
   char const * ex = arg( argc, argv, "expect", NULL );
   if( ex ) {
     FILE * fe = fopen( ex, "rb" );
     if( !fe ) { perror( ex ); return 2; }
-    L.expect.resize( n );
-    if( fread( L.expect.data(), 1, n, fe ) != n ) return 2;
+    expect.resize( n );
+    if( fread( expect.data(), 1, n, fe ) != n ) return 2;
     fclose( fe );
   }
-  (void)sigs_total;
   std::string mode = arg( argc, argv, "mode", "copy" );
-  L.inplace  = mode == "inplace";
-  L.depth    = strtoul( arg( argc, argv, "depth", "16384" ), NULL, 0 );
-  if( !L.depth || (L.depth & (L.depth - 1UL)) ) { fprintf( stderr, "depth: a power of 2\n" ); return 2; }
-  L.mask     = L.depth - 1UL;
-  L.credit   = atoi( arg( argc, argv, "credit", "0" ) );
-  L.rate     = atof( arg( argc, argv, "rate", "0" ) );
-  L.count    = strtoul( arg( argc, argv, "count", "0" ), NULL, 0 );
-  L.seconds  = atof( arg( argc, argv, "seconds", "5" ) );
-  double warm_s = atof( arg( argc, argv, "warm", "0" ) );
-  L.warm     = L.rate > 0. ? (unsigned long)( warm_s * L.rate ) : 0UL;
+  int const     inplace  = mode == "inplace";
+  unsigned long depth    = strtoul( arg( argc, argv, "depth", "16384" ), NULL, 0 );
+  if( !depth || (depth & (depth - 1UL)) ) { fprintf( stderr, "depth: a power of 2\n" ); return 2; }
+  int const     credit   = atoi( arg( argc, argv, "credit", "0" ) );
+  double const  rate     = atof( arg( argc, argv, "rate", "0" ) );        /* frags/s per tile */
+  unsigned long count    = strtoul( arg( argc, argv, "count", "0" ), NULL, 0 );
+  double const  seconds  = atof( arg( argc, argv, "seconds", "5" ) );
+  double const  warm_s   = atof( arg( argc, argv, "warm", "0" ) );
   unsigned long batch    = strtoul( arg( argc, argv, "batch", "4096" ), NULL, 0 );
   int           edepth   = atoi( arg( argc, argv, "eng_depth", "8" ) );
   long          max_wait = strtol( arg( argc, argv, "max_wait_ns", "0" ), NULL, 0 );
   long          lazy     = strtol( arg( argc, argv, "lazy_ns", "0" ), NULL, 0 );
   int           device   = atoi( arg( argc, argv, "device", "0" ) );
   char const *  pubout   = arg( argc, argv, "pubout", NULL );
-  char const *  cpus     = arg( argc, argv, "cpus", NULL );   /* "producer,tile" */
+  char const *  cpus     = arg( argc, argv, "cpus", NULL );   /* "producer0,tile0,producer1,tile1,..." */
+  int const     tiles    = atoi( arg( argc, argv, "tiles", "1" ) );   /* independent tiles on the device, one link each */
+  int const     use_ovrn = atoi( arg( argc, argv, "ovrn", "1" ) );
+  if( tiles < 1 || tiles > 8 || (pubout && tiles > 1) ) { fprintf( stderr, "tiles: 1..8 (pubout: one tile)\n" ); return 2; }
 #ifdef VT_LIVE_FAKE
   fake_engine_cheap_default( atoi( arg( argc, argv, "cheap", "0" ) ) );
 #endif
+  int cl[16]; int ncl = 0;
+  for( char const * c = cpus; c && *c && ncl < 16; ) { cl[ncl++] = atoi( c ); c = strchr( c, ',' ); if( c ) c++; }
 
-  /* the link */
   unsigned long chunk_sz = ( fmax + 63UL ) & ~63UL;
-  L.dc_sz = ( L.depth + 4UL ) * chunk_sz;
-  L.mc = new line_t[ L.depth ];
-  for( unsigned long i=0; i<L.depth; i++ ) L.mc[i].seq.store( i - L.depth, std::memory_order_relaxed );   /* "old" */
-  if( posix_memalign( (void **)&L.dc, 4096UL, L.dc_sz ) ) return 3;
-  memset( L.dc, 0, L.dc_sz );
-  L.out_sz = 64UL << 20;
-  L.out = (unsigned char *)malloc( L.out_sz );
-  L.lat = (fd_verify_tile_lat_t *)calloc( 1, sizeof(fd_verify_tile_lat_t) );
-  L.pubout = pubout ? fopen( pubout, "wb" ) : NULL;
-  L.fseq.store( 0 ); L.stop.store( 0 ); L.produced.store( 0 ); L.want_a.store( 0 ); L.pub_a.store( 0 ); L.taken_a.store( 0 );
-
-  /* the task (init before any sandbox would close syscalls) */
-  static fd_verify_tile_cnc_t cnc; memset( &cnc, 0, sizeof(cnc) );
-  static fd_verify_tile_args_t a; memset( &a, 0, sizeof(a) );
-  a.device = device; a.max_sigs = batch; a.max_blob = batch * 1536UL; a.depth = edepth;
-  a.cfg.batch_sigs = batch; a.cfg.tcache_depth = 16; a.cfg.tcache_map_cnt = 64; a.cfg.max_wait_ns = max_wait;
-  a.cnc = &cnc; a.in_seq = in_seq; a.in_ctx = &L; a.publish = publish; a.pub_ctx = &L;
-  a.lazy_ns = lazy;
-  /* ovrn=0: no overrun checks (a control: the byte check must then catch
-     the overwritten frags an overrun producer leaves in place) */
-  if( atoi( arg( argc, argv, "ovrn", "1" ) ) ) { a.ovrn = ovrn; a.chunk = chunk; a.ovrn_ctx = &L; }
-  if( L.inplace ) { a.region = L.dc; a.region_sz = L.dc_sz; }
-  L.args = &a;
+  std::vector<tile_run *> T( (size_t)tiles );
   fd_verify_tile_task_t const * task = fd_verify_tile_task_get();
-  sig_store( &cnc, FD_VERIFY_TILE_SIGNAL_BOOT );
-  task->init( &a );
-  if( a.err ) { printf( "{\"error\": \"init\", \"err\": %d}\n", a.err ); return 4; }
+  for( int k=0; k<tiles; k++ ) {
+    tile_run * tr = T[k] = new tile_run();
+    live & L = tr->L;
+    L.fragp = &corpus; L.expectp = &expect; L.n = n;
+    L.inplace = inplace; L.depth = depth; L.mask = depth - 1UL; L.credit = credit;
+    L.rate = rate; L.count = count; L.seconds = seconds;
+    L.pf = strtoul( arg( argc, argv, "pf", "4" ), NULL, 0 );
+    L.warm = rate > 0. ? (unsigned long)( warm_s * rate ) : 0UL;
+    /* the link */
+    L.dc_sz = ( L.depth + 4UL ) * chunk_sz;
+    L.mc = new line_t[ L.depth ];
+    for( unsigned long i=0; i<L.depth; i++ ) L.mc[i].seq.store( i - L.depth, std::memory_order_relaxed );   /* "old" */
+    if( posix_memalign( (void **)&L.dc, 4096UL, L.dc_sz ) ) return 3;
+    memset( L.dc, 0, L.dc_sz );
+    L.out_sz = 64UL << 20;
+    L.out = (unsigned char *)malloc( L.out_sz );
+    L.lat = (fd_verify_tile_lat_t *)calloc( 1, sizeof(fd_verify_tile_lat_t) );
+    L.pubout = pubout ? fopen( pubout, "wb" ) : NULL;
+    L.fseq.store( 0 ); L.stop.store( 0 ); L.produced.store( 0 ); L.want_a.store( 0 ); L.pub_a.store( 0 ); L.taken_a.store( 0 );
+    /* the task (init before any sandbox would close syscalls) */
+    fd_verify_tile_args_t & a = tr->a;
+    memset( &tr->cnc, 0, sizeof(tr->cnc) ); memset( &a, 0, sizeof(a) );
+    a.device = device; a.max_sigs = batch; a.max_blob = batch * 1536UL; a.depth = edepth;
+    a.cfg.batch_sigs = batch; a.cfg.tcache_depth = 16; a.cfg.tcache_map_cnt = 64; a.cfg.max_wait_ns = max_wait;
+    a.cnc = &tr->cnc; a.in_seq = in_seq; a.in_ctx = &L; a.publish = publish; a.pub_ctx = &L;
+    a.lazy_ns = lazy;
+    /* ovrn=0: no overrun checks (a control: the byte check must then catch
+       the overwritten frags an overrun producer leaves in place) */
+    if( use_ovrn ) { a.ovrn = ovrn; a.chunk = chunk; a.ovrn_ctx = &L; }
+    if( L.inplace ) { a.region = L.dc; a.region_sz = L.dc_sz; }
+    L.args = &a;
+    sig_store( &tr->cnc, FD_VERIFY_TILE_SIGNAL_BOOT );
+    task->init( &a );
+    if( a.err ) { printf( "{\"error\": \"init\", \"err\": %d, \"tile\": %d}\n", a.err, k ); return 4; }
 #ifdef VT_LIVE_FAKE
-  fake_engine_speed( a.gpu, strtoul( arg( argc, argv, "fake_ns_per_sig", "0" ), NULL, 0 ) );   /* a modelled device's pace */
+    fake_engine_speed( a.gpu, strtoul( arg( argc, argv, "fake_ns_per_sig", "0" ), NULL, 0 ) );   /* a modelled device's pace */
 #endif
-  int cpu_p = -1, cpu_t = -1;
-  if( cpus ) sscanf( cpus, "%d,%d", &cpu_p, &cpu_t );
+    tr->cpu_p = 2*k   < ncl ? cl[2*k]   : -1;
+    tr->cpu_t = 2*k+1 < ncl ? cl[2*k+1] : -1;
+  }
 
   unsigned long t_start = now_ns();
-  std::thread run( [&]() {
-    if( cpu_t >= 0 ) { cpu_set_t m; CPU_ZERO( &m ); CPU_SET( cpu_t, &m ); sched_setaffinity( 0, sizeof(m), &m ); }
-    task->run( &a );
-  } );
-  int ok = wait_signal( &cnc, FD_VERIFY_TILE_SIGNAL_RUN, 30. );
-  std::thread prod( [&]() {
-    if( cpu_p >= 0 ) { cpu_set_t m; CPU_ZERO( &m ); CPU_SET( cpu_p, &m ); sched_setaffinity( 0, sizeof(m), &m ); }
-    if( ok ) producer( &L );
-  } );
-  prod.join();
-  /* let the consumer catch up with the producer (bounded), then HALT --
-     the only signal the task gets; publishes before it are the run loop's */
-  unsigned long produced = L.produced.load(), t_wait = now_ns();
-  unsigned long taken_at_end = 0;
-  for(;;) {
-    if( sig_load( &cnc ) != FD_VERIFY_TILE_SIGNAL_RUN ) break;
-    taken_at_end = L.want_a.load( std::memory_order_relaxed );
-    if( taken_at_end >= produced || now_ns() - t_wait > 5000000000UL ) break;
-    struct timespec t = { 0, 200000L }; nanosleep( &t, NULL );
-  }
-  /* wait (bounded: settle_s) until the run loop has accounted for every
-     frag it took -- published, filtered or dropped, per the diagnostics
-     it pushes to the cnc at housekeeping -- then HALT: publishes that
-     happened before HALT are the liveness check (a tile that holds a
-     partial batch until HALT never gets there) */
-  unsigned long t_drain = now_ns();
+  std::vector<std::thread> runs, prods;
+  for( int k=0; k<tiles; k++ ) runs.emplace_back( [&, k]() { pin( T[k]->cpu_t ); task->run( &T[k]->a ); } );
+  int ok = 1;
+  for( int k=0; k<tiles; k++ ) ok &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_RUN, 30. );
+  for( int k=0; k<tiles; k++ ) prods.emplace_back( [&, k]() { pin( T[k]->cpu_p ); if( ok ) producer( &T[k]->L ); } );
+  for( auto & th : prods ) th.join();
+  /* let each consumer catch up with its producer (bounded), then wait
+     (bounded: settle_s) until the run loop has accounted for every frag
+     it took -- published, filtered or dropped, per the diagnostics it
+     pushes to the cnc at housekeeping -- then HALT: the only signal a task
+     gets; publishes that happened before HALT are the liveness check (a
+     tile that holds a partial batch until HALT never gets there) */
+  unsigned long t_wait = now_ns();
   double settle_s = atof( arg( argc, argv, "settle_s", "10" ) );
-  for(;;) {
-    unsigned long acc = 0;
-    unsigned long const ks[] = { FD_VERIFY_TILE_DIAG_PUB_CNT, FD_VERIFY_TILE_DIAG_SV_FILT_CNT, FD_VERIFY_TILE_DIAG_HA_FILT_CNT,
-                                 FD_VERIFY_TILE_DIAG_BAD_CNT, FD_VERIFY_TILE_DIAG_OVRN_CNT };
-    for( unsigned long k : ks ) acc += __atomic_load_n( &cnc.diag[k], __ATOMIC_RELAXED );
-    if( acc >= L.taken_a.load( std::memory_order_relaxed ) ) break;
-    if( sig_load( &cnc ) != FD_VERIFY_TILE_SIGNAL_RUN || (double)(now_ns() - t_drain) > settle_s * 1e9 ) break;
-    struct timespec t = { 0, 200000L }; nanosleep( &t, NULL );
+  for( int k=0; k<tiles; k++ ) {
+    live & L = T[k]->L;
+    unsigned long produced = L.produced.load();
+    for(;;) {
+      if( sig_load( &T[k]->cnc ) != FD_VERIFY_TILE_SIGNAL_RUN ) break;
+      if( L.want_a.load( std::memory_order_relaxed ) >= produced || now_ns() - t_wait > 5000000000UL ) break;
+      struct timespec t = { 0, 200000L }; nanosleep( &t, NULL );
+    }
+  }
+  unsigned long t_drain = now_ns();
+  for( int k=0; k<tiles; k++ ) {
+    for(;;) {
+      unsigned long acc = 0;
+      unsigned long const ks[] = { FD_VERIFY_TILE_DIAG_PUB_CNT, FD_VERIFY_TILE_DIAG_SV_FILT_CNT, FD_VERIFY_TILE_DIAG_HA_FILT_CNT,
+                                   FD_VERIFY_TILE_DIAG_BAD_CNT, FD_VERIFY_TILE_DIAG_OVRN_CNT };
+      for( unsigned long c : ks ) acc += __atomic_load_n( &T[k]->cnc.diag[c], __ATOMIC_RELAXED );
+      if( acc >= T[k]->L.taken_a.load( std::memory_order_relaxed ) ) break;
+      if( sig_load( &T[k]->cnc ) != FD_VERIFY_TILE_SIGNAL_RUN || (double)(now_ns() - t_drain) > settle_s * 1e9 ) break;
+      struct timespec t = { 0, 200000L }; nanosleep( &t, NULL );
+    }
   }
   t_drain = now_ns();
-  unsigned long pub_before_halt = L.pub_a.load( std::memory_order_relaxed );
-  sig_store( &cnc, FD_VERIFY_TILE_SIGNAL_HALT );
-  int booted = wait_signal( &cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
-  L.stop.store( 1 );
-  run.join();
+  unsigned long pub_before_halt = 0;
+  for( int k=0; k<tiles; k++ ) pub_before_halt += T[k]->L.pub_a.load( std::memory_order_relaxed );
+  int booted = 1, err = 0;
+  for( int k=0; k<tiles; k++ ) sig_store( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_HALT );
+  for( int k=0; k<tiles; k++ ) booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
+  for( int k=0; k<tiles; k++ ) T[k]->L.stop.store( 1 );
+  for( auto & th : runs ) th.join();
   unsigned long t_end = now_ns();
-  unsigned long d[ FD_VERIFY_TILE_DIAG_CNT ];
-  for( unsigned long k=0; k<FD_VERIFY_TILE_DIAG_CNT; k++ ) d[k] = cnc.diag[k];
-  if( L.pubout ) fclose( L.pubout );
-  double el = (double)( L.t_prod1 - L.t_prod0 ) * 1e-9;
+
+  /* the tiles summed */
+  unsigned long d[ FD_VERIFY_TILE_DIAG_CNT ] = { 0 };
+  static fd_verify_tile_lat_t lat;
+  memset( &lat, 0, sizeof(lat) );
+  unsigned long produced = 0, taken = 0, ovrnp = 0, ovrnr = 0, pub = 0, pub_sz = 0, mismatch = 0, false_pub = 0, order_err = 0, tpe = 0;
+  unsigned long tp0 = ~0UL, tp1 = 0;
+  for( int k=0; k<tiles; k++ ) {
+    live & L = T[k]->L;
+    for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ ) d[c] += T[k]->cnc.diag[c];
+    lat.cnt += L.lat->cnt; lat.sum_ns += L.lat->sum_ns; lat.over += L.lat->over;
+    if( L.lat->max_ns > lat.max_ns ) lat.max_ns = L.lat->max_ns;
+    for( unsigned long b=0; b<FD_VERIFY_TILE_LAT_BINS; b++ ) lat.bin[b] += L.lat->bin[b];
+    produced += L.produced.load(); taken += L.taken; ovrnp += L.ovrnp; ovrnr += L.ovrnr; pub += L.pub; pub_sz += L.pub_sz;
+    mismatch += L.mismatch; false_pub += L.false_pub; order_err += L.order_err; tpe += L.taken_pass_expected;
+    if( L.t_prod0 < tp0 ) tp0 = L.t_prod0;
+    if( L.t_prod1 > tp1 ) tp1 = L.t_prod1;
+    err |= T[k]->a.err;
+    if( L.pubout ) fclose( L.pubout );
+  }
+  double el = tp1 > tp0 ? (double)( tp1 - tp0 ) * 1e-9 : 0.;
   double sigs_per_frag = 0.;
   {
-    /* signatures of the frags taken (from their txn trailers) */
+    /* signatures of the corpus's frags (from their txn trailers) */
     unsigned long ns = 0;
     for( unsigned i=0; i<n; i++ ) {
-      std::vector<unsigned char> const & f = L.frag[i];
+      std::vector<unsigned char> const & f = corpus[i];
       if( f.size() < 2 ) continue;
       unsigned long psz = (unsigned long)f[ f.size()-2 ] | ((unsigned long)f[ f.size()-1 ] << 8);
       unsigned long toff = ( psz + 1UL ) & ~1UL;
@@ -377,7 +434,7 @@ int main( int argc, char ** argv ) {
     }
     sigs_per_frag = (double)ns / (double)n;
   }
-  printf( "{\"mode\": \"%s\", \"credit\": %d, \"depth\": %lu, \"dcache_bytes\": %lu, \"batch_sigs\": %lu, \"eng_depth\": %d, "
+  printf( "{\"mode\": \"%s\", \"tiles\": %d, \"credit\": %d, \"depth\": %lu, \"dcache_bytes\": %lu, \"batch_sigs\": %lu, \"eng_depth\": %d, "
           "\"max_wait_ns\": %ld, \"rate_frags_s\": %.1f, \"corpus\": %u, \"sigs_per_frag\": %.4f, "
           "\"produced\": %lu, \"taken\": %lu, \"producer_s\": %.6f, \"offered_frags_s\": %.1f, "
           "\"taken_sigs_s\": %.1f, \"published_frags_s\": %.1f, \"drain_s\": %.6f, \"run_s\": %.6f, "
@@ -385,18 +442,30 @@ int main( int argc, char ** argv ) {
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
           "\"diag\": [",
-          L.inplace ? "inplace" : "copy", L.credit, L.depth, L.dc_sz, batch, edepth, max_wait, L.rate, n, sigs_per_frag,
-          produced, L.taken, el, el > 0. ? (double)produced / el : 0.,
-          el > 0. ? (double)d[ FD_VERIFY_TILE_DIAG_SIG_CNT ] / el : 0., el > 0. ? (double)L.pub / el : 0.,
+          inplace ? "inplace" : "copy", tiles, credit, depth, T[0]->L.dc_sz, batch, edepth, max_wait, rate, n, sigs_per_frag,
+          produced, taken, el, el > 0. ? (double)produced / el : 0.,
+          el > 0. ? (double)d[ FD_VERIFY_TILE_DIAG_SIG_CNT ] / el : 0., el > 0. ? (double)pub / el : 0.,
           (double)( t_drain - t_wait ) * 1e-9, (double)( t_end - t_start ) * 1e-9,   /* drain_s: catch-up + settle */
-          L.ovrnp, L.ovrnr, L.pub, pub_before_halt, L.pub_sz, L.mismatch, L.false_pub, L.order_err, L.taken_pass_expected,
-          booted, a.err,
-          L.lat->cnt, L.lat->cnt ? (double)L.lat->sum_ns / (double)L.lat->cnt * 1e-6 : -1., pct_ms( L.lat, .5 ), pct_ms( L.lat, .99 ),
-          pct_ms( L.lat, .999 ), (double)L.lat->max_ns * 1e-6 );
+          ovrnp, ovrnr, pub, pub_before_halt, pub_sz, mismatch, false_pub, order_err, tpe, booted, err,
+          lat.cnt, lat.cnt ? (double)lat.sum_ns / (double)lat.cnt * 1e-6 : -1., pct_ms( &lat, .5 ), pct_ms( &lat, .99 ),
+          pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6 );
   for( unsigned long k=0; k<FD_VERIFY_TILE_DIAG_CNT; k++ ) printf( "%s%lu", k ? ", " : "", d[k] );
   printf( "]}\n" );
+#ifdef FD_VT_PROF
+  {  /* profiling builds: the tile's per-phase TSC cycles (fd_verify_tile.cpp FD_VT_PROF) */
+    extern unsigned long fd_vt_prof[8];
+    fprintf( stderr, "fd_vt_prof cycles/frag: trailer %.1f tcache %.1f reserve %.1f copy %.1f desc %.1f | publish/batch %.0f | frags %lu batches %lu\n",
+             (double)fd_vt_prof[0]/(double)fd_vt_prof[6], (double)fd_vt_prof[1]/(double)fd_vt_prof[6], (double)fd_vt_prof[2]/(double)fd_vt_prof[6],
+             (double)fd_vt_prof[3]/(double)fd_vt_prof[6], (double)fd_vt_prof[4]/(double)fd_vt_prof[6], (double)fd_vt_prof[5]/(double)(fd_vt_prof[7]+1),
+             fd_vt_prof[6], fd_vt_prof[7] );
+  }
+#endif
   fflush( stdout );
-  task->fini( &a );
-  delete [] L.mc; free( L.dc ); free( L.out ); free( L.lat );
-  return booted && !a.err ? 0 : 1;
+  for( int k=0; k<tiles; k++ ) {
+    task->fini( &T[k]->a );
+    live & L = T[k]->L;
+    delete [] L.mc; free( L.dc ); free( L.out ); free( L.lat );
+    delete T[k];
+  }
+  return booted && !err ? 0 : 1;
 }

@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--eng-depth", type=int, default=8)
     ap.add_argument("--depth", type=int, default=16384, help="mcache/dcache frags (default.toml receive_buffer_size)")
     ap.add_argument("--max-wait-ns", type=int, default=0)
+    ap.add_argument("--tiles", type=int, default=1, help="verify tiles on the GPU, each with its own link and producer")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -74,12 +75,13 @@ def main():
     write_frags(fp, frags)
     ok.astype(np.uint8).tofile(ex)
     cpus = fa.numa_cpus(0)
-    pin = f"{cpus[0]},{cpus[1]}" if len(cpus) >= 2 else None
+    # producer k and tile k on distinct CPUs of the GPU's NUMA node
+    pin = ",".join(str(c) for c in cpus[:2 * a.tiles]) if len(cpus) >= 2 * a.tiles else None
     exe = os.path.join(ROOT, "firedancer_amd", "vt_live")
     out = open(a.out, "a") if a.out else None
     for mode in a.modes.split(","):
         for r in [float(x) for x in a.rates.split(",")]:
-            kw = dict(mode=mode, rate=r / spf, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
+            kw = dict(mode=mode, rate=r / spf / a.tiles, tiles=a.tiles, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
                       eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex)
             if pin:
                 kw["cpus"] = pin
