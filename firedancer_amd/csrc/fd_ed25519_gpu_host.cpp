@@ -602,10 +602,11 @@ static void fd_abandon_ticket( fd_ed25519_gpu_t * g, unsigned long ticket ) {
    slot as it would have without the early return.  Caller holds g->lock.
    Returns 1 if a slot came back. */
 /* the bound on that wait under the lock: a retiring slot's event follows
-   its codes within microseconds; one that has not fired by then (a wedged
-   device) is left for later rather than stalling every engine caller for
+   its codes within microseconds (hundreds under a loaded device); one that
+   has not fired within 2 ms (a wedged device) is left for later -- the
+   caller sees a full ring -- rather than stalling every engine caller for
    the whole engine timeout */
-#define FD_RETIRE_WAIT_NS 200000L
+#define FD_RETIRE_WAIT_NS 2000000L
 static int fd_wait_retiring( fd_ed25519_gpu_t * g ) {
   for( int s=0; s<g->depth; s++ )
     if( g->slot[s].retiring ) {

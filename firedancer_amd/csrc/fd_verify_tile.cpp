@@ -322,6 +322,23 @@ static int fd_vt_wait_any( fd_verify_tile_t * t ) {
   }
 }
 
+/* The ring is full but none of its slots holds a batch of this tile
+   (another tile's batches on a shared engine, or slots whose codes a poll
+   took early and whose completion event has not fired yet): wait for a
+   slot with short sleeps, bounded by the engine timeout, instead of
+   failing the tile.  try() returns nonzero once it got one. */
+template<typename TRY>
+static int fd_vt_wait_slot( fd_verify_tile_t * t, TRY try_ ) {
+  long to = fd_ed25519_gpu_timeout( t->gpu );
+  unsigned long t0 = fd_vt_now();
+  for(;;) {
+    int r = try_();
+    if( r ) return r;
+    if( to >= 0 && fd_vt_now() - t0 > (unsigned long)to ) return FD_ED25519_ERR_GPU;
+    struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL );
+  }
+}
+
 static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
   if( !b || !b->nsig ) return 0;
@@ -330,11 +347,19 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
     for(;;) {
-      int r = b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, b->desc, &b->ticket )
-                      : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+      auto try_ = [&]() {
+        return b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, b->desc, &b->ticket )
+                       : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+      };
+      int r = try_();
       if( r == 1 ) break;
-      if( r < 0 || t->inflight.empty() ) return FD_ED25519_ERR_GPU;
+      if( r < 0 ) return FD_ED25519_ERR_GPU;
       t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
+      if( t->inflight.empty() ) {
+        r = fd_vt_wait_slot( t, try_ );
+        if( r == 1 ) break;
+        return FD_ED25519_ERR_GPU;
+      }
       int err = fd_vt_drain( t, 1 );
       if( err ) return err;
     }
@@ -432,7 +457,14 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
       }
     } else {
       void * blob; fd_ed25519_gpu_desc_t * desc;
-      if( !fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ) {
+      auto try_ = [&]() { return fd_ed25519_gpu_stage( t->gpu, &blob, &desc ) ? 0 : 1; };
+      int got = try_();
+      if( !got && t->inflight.empty() ) {
+        t->diag[ FD_VERIFY_TILE_DIAG_RING_FULL_CNT ]++;
+        if( fd_vt_wait_slot( t, try_ ) != 1 ) return FD_ED25519_ERR_GPU;
+        got = 1;
+      }
+      if( got ) {
         fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
         b->blob = (uint8_t *)blob; b->desc = desc; b->used = 0; b->nsig = 0; b->ticket = 0;
         t->open = b;

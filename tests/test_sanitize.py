@@ -191,8 +191,9 @@ def test_tile_task_live_producer_asan_and_tsan(built, ref, tmp_path):
     for mode in ("copy", "inplace"):
         for rate in (1000, 1_000_000):
             po = str(tmp_path / f"pub_{mode}_{rate}.bin")
+            cpus = sorted(os.sched_getaffinity(0))
             d = _live(built, "san_live", p, env, mode=mode, rate=rate, count=len(frags), depth=16384, batch=512,
-                      eng_depth=3, pubout=po, cheap=1)
+                      eng_depth=3, pubout=po, cheap=1, **({"cpus": f"{cpus[0]},{cpus[2]}"} if len(cpus) >= 3 else {}))
             assert d["rc"] == 0 and d["taken"] == len(frags) and d["diag"]["OVRN_CNT"] == 0, (mode, rate, d)
             pub = read_pubout(po)
             assert [frags[int(s)] for s in pub[:, 0]] == exp_pub, (mode, rate)

@@ -395,8 +395,15 @@ int main( int argc, char ** argv ) {
   unsigned long pub_before_halt = 0;
   for( int k=0; k<tiles; k++ ) pub_before_halt += T[k]->L.pub_a.load( std::memory_order_relaxed );
   int booted = 1, err = 0;
-  for( int k=0; k<tiles; k++ ) sig_store( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_HALT );
-  for( int k=0; k<tiles; k++ ) booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
+  /* a task that failed has returned: its FAIL stays (HALT goes only to a
+     running task) */
+  int running[8];
+  for( int k=0; k<tiles; k++ ) {
+    running[k] = sig_load( &T[k]->cnc ) == FD_VERIFY_TILE_SIGNAL_RUN;
+    if( running[k] ) sig_store( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_HALT );
+    else booted = 0;
+  }
+  for( int k=0; k<tiles; k++ ) if( running[k] ) booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
   for( int k=0; k<tiles; k++ ) T[k]->L.stop.store( 1 );
   for( auto & th : runs ) th.join();
   unsigned long t_end = now_ns();
