@@ -632,15 +632,15 @@ extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25
   return FD_ED25519_ERR_ARG;
 }
 
+/* A stage is released exactly once, by its owner: unstage, a submit of
+   its blob, or a failed submit of it (which releases it under the same
+   lock hold, so a slot orphaned by that failure is never seen staged by
+   fd_reclaim_orphans and lent to a second caller while the first still
+   holds it -- ADVICE r05). */
 extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
   if( !g ) return;
   std::lock_guard<std::mutex> guard( g->lock );
-  /* only a slot still lent out and idle: a failed submit may have
-     orphaned it meanwhile, and once reclaimed and lent to another caller
-     that caller's stage must not be cleared by this late unstage
-      */
-  for( int s=0; s<g->depth; s++ )
-    if( g->slot[s].h_blob == blob && !g->slot[s].ticket && !g->slot[s].orphan ) g->slot[s].staged = 0;
+  for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) g->slot[s].staged = 0;
 }
 
 /* a free slot: the staged one owning `blob` if any, else any unstaged one
@@ -954,8 +954,8 @@ extern "C" int fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t * g, unsigned long n
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
   if( !sl ) return 0;                    /* ring full: poll first */
   int err = fd_slot_enqueue( g, sl, n, blob, blob_sz, desc, blob2, blob2_sz );
+  sl->staged = 0;                        /* released, submitted or not (fd_ed25519_gpu_unstage) */
   if( err ) return err;
-  sl->staged = 0;
   sl->ticket = g->next_ticket++;
   *ticket = sl->ticket;
   return 1;
@@ -998,7 +998,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
-  if( block && sl->early && out ) {   /* a drain (out NULL) waits for the event */
+  if( (block & 1) && sl->early && out ) {   /* a drain (out NULL) waits for the event */
     fd_codes_ctx c = { sl, 1u };
     int r = fd_wait_query( fd_codes_query, &c, FD_POLL_SPIN_NS, fd_timeout( g ) );
     if( r < 0 ) return FD_ED25519_ERR_GPU;
@@ -1011,9 +1011,10 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
       std::lock_guard<std::mutex> guard( g->lock );
       if( out ) fd_slot_collect( sl, out );
       sl->early = 0; sl->retiring = 1;
+      if( block & FD_ED25519_GPU_POLL_KEEP ) sl->staged = 1;   /* its pinned buffers stay the caller's */
       return 1;
     }
-  } else if( block ) {
+  } else if( block & 1 ) {
     int err = fd_event_wait( sl->done, fd_timeout( g ) );
     if( err ) return err;               /* timed out or failed; the ticket stays valid */
   } else {
@@ -1024,6 +1025,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   std::lock_guard<std::mutex> guard( g->lock );
   if( out ) fd_slot_collect( sl, out );
   sl->ticket = 0; sl->early = 0;
+  if( block & FD_ED25519_GPU_POLL_KEEP ) sl->staged = 1;   /* lent back to the caller (unstage to free) */
   return 1;
 }
 
@@ -1417,7 +1419,7 @@ static int fd_run_ptr_short( fd_ed25519_gpu_t * g, unsigned long n, uint8_t cons
     }
     unsigned long ticket = 0;
     int r = fd_ed25519_gpu_try_submit( g, cnt, hb, used, dd, &ticket );
-    if( r != 1 ) { fd_ed25519_gpu_unstage( g, hb ); return r < 0 ? r : FD_ED25519_ERR_GPU; }
+    if( r != 1 ) { if( !r ) fd_ed25519_gpu_unstage( g, hb ); return r < 0 ? r : FD_ED25519_ERR_GPU; }   /* a failed submit released it */
     r = fd_ed25519_gpu_poll( g, ticket, out + i, 1 );
     if( r != 1 ) {
       /* timed out or failed: nobody polls this ticket again, so its slot is

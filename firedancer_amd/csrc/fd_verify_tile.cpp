@@ -227,7 +227,11 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
     if( st < 0 ) return FD_ED25519_ERR_GPU;
     codes = b->codes;
   } else {
-    int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), block );
+    /* copy mode publishes from the slot's pinned blob: keep it lent until
+       the publishes are done (an engine shared with other tiles would
+       otherwise hand the slot to one of them now) */
+    int const keep = t->inplace ? 0 : FD_ED25519_GPU_POLL_KEEP;
+    int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), (block ? 1 : 0) | keep );
     if( r <= 0 ) return r ? FD_ED25519_ERR_GPU : 0;
     codes = t->out.data();
   }
@@ -267,6 +271,7 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
 #ifdef FD_VT_PROF
   fd_vt_prof[7]++;
 #endif
+  if( !t->multi && !t->inplace ) fd_ed25519_gpu_unstage( t->gpu, b->blob );   /* the slot's blob back to the engine */
   b->txns.clear(); b->ticket = 0;
   t->pool.push_back( b );
   return 1;
@@ -383,7 +388,10 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
     t->next = (b->eng + 1) % t->gpu_cnt;   /* ties go round robin */
   } else {
     int err = fd_ed25519_gpu_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
-    if( err ) return FD_ED25519_ERR_GPU;
+    if( err ) {   /* the engine released the staged blob; the batch is gone */
+      b->txns.clear(); t->pool.push_back( b ); t->open = NULL;
+      return FD_ED25519_ERR_GPU;
+    }
   }
   t->diag[ FD_VERIFY_TILE_DIAG_BATCH_CNT ]++;
   t->inflight.push_back( b );

@@ -89,7 +89,7 @@ static void fd_vt_task_init( fd_verify_tile_args_t * a ) {
             : a->region ? fd_verify_tile_new_multi_inplace( a->gpus, (unsigned long)cnt, &a->cfg, a->region, a->region_sz, a->publish, a->pub_ctx )
             :             fd_verify_tile_new_multi( a->gpus, (unsigned long)cnt, &a->cfg, a->publish, a->pub_ctx );
   } else {
-    a->gpu  = fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, depth );
+    a->gpu  = a->shared_gpu ? a->shared_gpu : fd_ed25519_gpu_new_ex( a->device, a->max_sigs, a->max_blob, depth );
     if( a->gpu && a->region )   /* in place: frags DMA'd from the input dcache itself */
       a->tile = fd_verify_tile_new_inplace( a->gpu, &a->cfg, a->region, a->region_sz, a->publish, a->pub_ctx );
     else
@@ -185,7 +185,7 @@ static void fd_vt_task_fini( fd_verify_tile_args_t * a ) {
   if( a->device_cnt > 1 ) {
     int cnt = a->device_cnt > FD_VERIFY_TILE_GPU_MAX ? FD_VERIFY_TILE_GPU_MAX : a->device_cnt;
     for( int e=0; e<cnt; e++ ) { fd_ed25519_gpu_delete( a->gpus[e] ); a->gpus[e] = NULL; }
-  } else fd_ed25519_gpu_delete( a->gpu );
+  } else if( a->gpu != a->shared_gpu ) fd_ed25519_gpu_delete( a->gpu );
   a->gpu = NULL;
 }
 

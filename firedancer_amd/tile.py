@@ -200,7 +200,7 @@ class Args(ctypes.Structure):
                 ("device_cnt", ctypes.c_int), ("gpus", ctypes.c_void_p * GPU_MAX),
                 ("region", ctypes.c_void_p), ("region_sz", ctypes.c_ulong),
                 ("in_seq", ctypes.c_void_p), ("ovrn", ctypes.c_void_p), ("chunk", ctypes.c_void_p),
-                ("ovrn_ctx", ctypes.c_void_p)]
+                ("ovrn_ctx", ctypes.c_void_p), ("shared_gpu", ctypes.c_void_p)]
 
 
 class TaskFns(ctypes.Structure):

@@ -208,7 +208,8 @@ fd_ed25519_gpu_submit( fd_ed25519_gpu_t *            gpu,
 
 /* As fd_ed25519_gpu_submit, but a full ring is not an error: returns 1
    submitted (*ticket set), 0 no free slot (poll first), < 0 the batch
-   could not be run (FD_ED25519_ERR_ARG: bad arguments; FD_ED25519_ERR_GPU).
+   could not be run (FD_ED25519_ERR_ARG: bad arguments; FD_ED25519_ERR_GPU;
+   a staged blob is released either way: do not unstage it after).
    The per-GPU feeder submits through this, so a real argument error ends
    its job instead of being retried as "ring full". */
 int
@@ -240,6 +241,15 @@ fd_ed25519_gpu_poll( fd_ed25519_gpu_t * gpu,
                      unsigned long      ticket,
                      int *              out,
                      int                block );
+
+/* poll's block argument: bit 0 blocks (as above); FD_ED25519_GPU_POLL_KEEP
+   lends a completed batch's pinned staging buffers back to the caller (as
+   fd_ed25519_gpu_stage does) instead of freeing the slot, so bytes the
+   caller built in them stay its own until it calls fd_ed25519_gpu_unstage
+   (or submits them again) -- needed when several threads share an engine
+   and the caller still reads its batch after the codes are in (a verify
+   tile publishing frags from the slot it staged them in). */
+#define FD_ED25519_GPU_POLL_KEEP (2)
 
 int
 fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * gpu );

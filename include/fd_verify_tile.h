@@ -339,6 +339,12 @@ typedef struct {
   fd_verify_tile_ovrn_fn     ovrn;
   fd_verify_tile_chunk_fn    chunk;
   void *                     ovrn_ctx;
+  /* one engine shared by several tile tasks on a device (set by the
+     caller, optional; single-engine modes): init uses it instead of
+     creating one and fini leaves it to the caller.  The engine's ring
+     slots and CU groups are then shared by the tiles' batches, which keeps
+     two tiles on one GPU from stacking two rings on the same CU groups. */
+  fd_ed25519_gpu_t *         shared_gpu;
 } fd_verify_tile_args_t;
 
 typedef struct {

@@ -90,6 +90,7 @@ extern "C" unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * g ) {
 extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g->depth; }
 
 extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
+  std::lock_guard<std::mutex> l( g->lock );   /* an engine may be shared by several tiles (shared_gpu) */
   for( int s=0; s<g->depth; s++ ) {
     fake_slot * sl = &g->slot[s];
     if( !sl->ticket && !sl->staged ) { sl->staged = 1; *blob = sl->blob; *desc = sl->desc; return 0; }
@@ -97,6 +98,7 @@ extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25
   return FD_ED25519_ERR_ARG;
 }
 extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
+  std::lock_guard<std::mutex> l( g->lock );
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].blob == blob ) g->slot[s].staged = 0;
 }
 
@@ -108,7 +110,7 @@ extern "C" int fd_ed25519_gpu_try_submit( fd_ed25519_gpu_t * g, unsigned long n,
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && g->slot[s].blob == blob ) sl = &g->slot[s];
   for( int s=0; s<g->depth && !sl; s++ ) if( !g->slot[s].ticket && !g->slot[s].staged ) sl = &g->slot[s];
   if( !sl ) return 0;
-  if( g->fail_submit ) { int c = g->fail_submit; g->fail_submit = 0; return c; }
+  if( g->fail_submit ) { int c = g->fail_submit; g->fail_submit = 0; sl->staged = 0; return c; }   /* a failed submit releases a stage */
   if( sl->blob != blob ) memcpy( sl->blob, blob, blob_sz );
   if( sl->desc != desc ) memcpy( sl->desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   for( unsigned long i=0; i<n; i++ ) {
@@ -156,7 +158,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   if( wait_until ) {      /* the modelled device has not finished the batch yet */
     unsigned long now = fake_now();
     if( now < wait_until ) {
-      if( !block ) return 0;
+      if( !(block & 1) ) return 0;
       struct timespec ts = { (long)((wait_until - now) / 1000000000UL), (long)((wait_until - now) % 1000000000UL) };
       nanosleep( &ts, NULL );
     }
@@ -166,9 +168,10 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     fake_slot * sl = &g->slot[s];
     if( sl->ticket != ticket ) continue;
     if( sl->wedged ) return 0;                                   /* never completes */
-    if( !block && (ticket & 1UL) && !sl->polls++ ) return 0;   /* "still in flight" once */
+    if( !(block & 1) && (ticket & 1UL) && !sl->polls++ ) return 0;   /* "still in flight" once */
     if( out ) memcpy( out, sl->out, sl->n * sizeof(int) );
     sl->ticket = 0;
+    if( block & FD_ED25519_GPU_POLL_KEEP ) sl->staged = 1;   /* lent back to the caller */
     return 1;
   }
   return FD_ED25519_ERR_ARG;

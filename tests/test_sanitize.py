@@ -209,6 +209,16 @@ def test_tile_task_live_producer_asan_and_tsan(built, ref, tmp_path):
     assert ctl["rc"] == 0 and ctl["mismatch"] > 0, ctl       # unchecked, lapped frags go out overwritten
     d = _live(built, "san_live", p, env, **dict(kw, mode="copy"))
     assert d["rc"] == 0 and d["mismatch"] == 0 and d["ovrnp"] > 0, d
+    # two tiles sharing one engine (fd_verify_tile_args_t.shared_gpu): a
+    # completed batch's pinned blob stays the publishing tile's until it
+    # has published (FD_ED25519_GPU_POLL_KEEP) -- under ThreadSanitizer,
+    # both modes; every publish carries the bytes of its own seq
+    for mode in ("copy", "inplace"):
+        d = _live(built, "tsan_live", p, env, mode=mode, credit=1, rate=0, count=3 * len(frags), depth=256, batch=512,
+                  eng_depth=3, cheap=1, tiles=2, share=1)
+        assert d["rc"] == 0 and "ThreadSanitizer" not in d["stderr"], (mode, d["stderr"])
+        assert d["taken"] == 6 * len(frags) and d["mismatch"] == 0 and d["order_err"] == 0, (mode, d)
+        assert d["pub_before_halt"] == d["pub"] == 6 * len(exp_pub), (mode, d["pub"])
     # ThreadSanitizer: the credit-honouring link, both modes, as fast as it goes
     for mode in ("copy", "inplace"):
         po = str(tmp_path / f"tsan_{mode}.bin")

@@ -119,3 +119,29 @@ def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
     assert cred["taken"] == n and cred["ovrnp"] == 0 and cred["ovrnr"] == 0 and cred["diag"]["OVRN_CNT"] == 0, cred
     assert cred["mismatch"] == 0 and cred["false_pub"] == 0 and cred["pub"] == cred["taken_pass_expected"], cred
     assert cred["pub_before_halt"] == cred["pub"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["copy", "inplace"])
+def test_two_tiles_one_engine(ref, tmp_path, mode):
+    """Two verify tile tasks sharing one engine (fd_verify_tile_args_t.
+    shared_gpu), each with its own producer and link, at 10 M verifies/s
+    for 2 s: every publish carries exactly its seq's bytes and is one the
+    reference publishes, and nothing is lost (a copying tile publishes from
+    the ring slot it staged the frags in, kept lent past the poll,
+    FD_ED25519_GPU_POLL_KEEP)."""
+    frags, ok = _cyclic_corpus(ref, 20000, 73)
+    p = str(tmp_path / "frags.bin")
+    write_frags(p, frags)
+    ex = str(tmp_path / "expect.bin")
+    ok.astype(np.uint8).tofile(ex)
+    spf = np.mean([f[((int.from_bytes(f[-2:], "little") + 1) & ~1) + 1] for f in frags])
+    d = run(_exe(), p, mode=mode, rate=10e6 / spf / 2, seconds=2, tiles=2, share=1, depth=16384, batch=4096,
+            eng_depth=8, expect=ex, timeout=240, **({"cpus": _pin(4)} if _pin(4) else {}))
+    assert d["rc"] == 0 and d["booted"] == 1 and d["shared_engine"] == 1, d
+    assert d["mismatch"] == 0 and d["false_pub"] == 0 and d["order_err"] == 0, d
+    if d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0:
+        assert d["pub"] == d["taken_pass_expected"], d
+    assert d["pub_before_halt"] == d["pub"]
+    print(f"two tiles, one engine, {mode}: {d['taken_sigs_s'] / 1e6:.2f} M verifies/s, p50 {d['lat']['p50_ms']:.3f} "
+          f"p99 {d['lat']['p99_ms']:.3f} max {d['lat']['max_ms']:.3f} ms")

@@ -313,6 +313,12 @@ int main( int argc, char ** argv ) {
 
   unsigned long chunk_sz = ( fmax + 63UL ) & ~63UL;
   std::vector<tile_run *> T( (size_t)tiles );
+  /* share=1: one engine for all the tiles (fd_verify_tile_args_t.shared_gpu) */
+  fd_ed25519_gpu_t * shared = NULL;
+  if( atoi( arg( argc, argv, "share", "0" ) ) ) {
+    shared = fd_ed25519_gpu_new_ex( device, batch, batch * 1536UL, edepth );
+    if( !shared ) { printf( "{\"error\": \"shared engine\"}\n" ); return 4; }
+  }
   fd_verify_tile_task_t const * task = fd_verify_tile_task_get();
   for( int k=0; k<tiles; k++ ) {
     tile_run * tr = T[k] = new tile_run();
@@ -344,6 +350,7 @@ int main( int argc, char ** argv ) {
        the overwritten frags an overrun producer leaves in place) */
     if( use_ovrn ) { a.ovrn = ovrn; a.chunk = chunk; a.ovrn_ctx = &L; }
     if( L.inplace ) { a.region = L.dc; a.region_sz = L.dc_sz; }
+    a.shared_gpu = shared;
     L.args = &a;
     sig_store( &tr->cnc, FD_VERIFY_TILE_SIGNAL_BOOT );
     task->init( &a );
@@ -441,7 +448,7 @@ int main( int argc, char ** argv ) {
     }
     sigs_per_frag = (double)ns / (double)n;
   }
-  printf( "{\"mode\": \"%s\", \"tiles\": %d, \"credit\": %d, \"depth\": %lu, \"dcache_bytes\": %lu, \"batch_sigs\": %lu, \"eng_depth\": %d, "
+  printf( "{\"mode\": \"%s\", \"shared_engine\": %d, \"tiles\": %d, \"credit\": %d, \"depth\": %lu, \"dcache_bytes\": %lu, \"batch_sigs\": %lu, \"eng_depth\": %d, "
           "\"max_wait_ns\": %ld, \"rate_frags_s\": %.1f, \"corpus\": %u, \"sigs_per_frag\": %.4f, "
           "\"produced\": %lu, \"taken\": %lu, \"producer_s\": %.6f, \"offered_frags_s\": %.1f, "
           "\"taken_sigs_s\": %.1f, \"published_frags_s\": %.1f, \"drain_s\": %.6f, \"run_s\": %.6f, "
@@ -449,7 +456,7 @@ int main( int argc, char ** argv ) {
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
           "\"diag\": [",
-          inplace ? "inplace" : "copy", tiles, credit, depth, T[0]->L.dc_sz, batch, edepth, max_wait, rate, n, sigs_per_frag,
+          inplace ? "inplace" : "copy", shared ? 1 : 0, tiles, credit, depth, T[0]->L.dc_sz, batch, edepth, max_wait, rate, n, sigs_per_frag,
           produced, taken, el, el > 0. ? (double)produced / el : 0.,
           el > 0. ? (double)d[ FD_VERIFY_TILE_DIAG_SIG_CNT ] / el : 0., el > 0. ? (double)pub / el : 0.,
           (double)( t_drain - t_wait ) * 1e-9, (double)( t_end - t_start ) * 1e-9,   /* drain_s: catch-up + settle */
@@ -470,6 +477,7 @@ int main( int argc, char ** argv ) {
   fflush( stdout );
   for( int k=0; k<tiles; k++ ) {
     task->fini( &T[k]->a );
+    if( k == tiles - 1 && shared ) fd_ed25519_gpu_delete( shared );
     live & L = T[k]->L;
     delete [] L.mc; free( L.dc ); free( L.out ); free( L.lat );
     delete T[k];

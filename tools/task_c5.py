@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--depth", type=int, default=16384, help="mcache/dcache frags (default.toml receive_buffer_size)")
     ap.add_argument("--max-wait-ns", type=int, default=0)
     ap.add_argument("--tiles", type=int, default=1, help="verify tiles on the GPU, each with its own link and producer")
+    ap.add_argument("--share", type=int, default=0, help="1: the tiles share one engine (fd_verify_tile_args_t.shared_gpu)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -81,7 +82,7 @@ def main():
     out = open(a.out, "a") if a.out else None
     for mode in a.modes.split(","):
         for r in [float(x) for x in a.rates.split(",")]:
-            kw = dict(mode=mode, rate=r / spf / a.tiles, tiles=a.tiles, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
+            kw = dict(mode=mode, rate=r / spf / a.tiles, tiles=a.tiles, share=a.share, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
                       eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex)
             if pin:
                 kw["cpus"] = pin
