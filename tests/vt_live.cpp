@@ -362,6 +362,12 @@ int main( int argc, char ** argv ) {
     tr->cpu_t = 2*k+1 < ncl ? cl[2*k+1] : -1;
   }
 
+#ifndef VT_LIVE_FAKE
+  /* the shader clock the DSM waves ran at over the run (per device sums):
+     at light load the device may hold a low clock, which lengthens every
+     batch */
+  fd_ed25519_gpu_dsm_clock( T[0]->a.gpu, 1, NULL );
+#endif
   unsigned long t_start = now_ns();
   std::vector<std::thread> runs, prods;
   for( int k=0; k<tiles; k++ ) runs.emplace_back( [&, k]() { pin( T[k]->cpu_t ); task->run( &T[k]->a ); } );
@@ -411,6 +417,10 @@ int main( int argc, char ** argv ) {
     else booted = 0;
   }
   for( int k=0; k<tiles; k++ ) if( running[k] ) booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
+  unsigned long long clk[9] = { 0 };
+#ifndef VT_LIVE_FAKE
+  if( shared || tiles == 1 ) fd_ed25519_gpu_dsm_clock( shared ? shared : T[0]->a.gpu, 0, clk );
+#endif
   for( int k=0; k<tiles; k++ ) T[k]->L.stop.store( 1 );
   for( auto & th : runs ) th.join();
   unsigned long t_end = now_ns();
@@ -455,6 +465,7 @@ int main( int argc, char ** argv ) {
           "\"ovrnp\": %lu, \"ovrnr\": %lu, \"pub\": %lu, \"pub_before_halt\": %lu, \"pub_sz\": %lu, "
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
+          "\"dsm_ghz\": {\"pool\": %.3f, \"quad\": %.3f, \"oct\": %.3f}, \"dsm_waves\": [%llu, %llu, %llu], "
           "\"diag\": [",
           inplace ? "inplace" : "copy", shared ? 1 : 0, tiles, credit, depth, T[0]->L.dc_sz, batch, edepth, max_wait, rate, n, sigs_per_frag,
           produced, taken, el, el > 0. ? (double)produced / el : 0.,
@@ -462,7 +473,9 @@ int main( int argc, char ** argv ) {
           (double)( t_drain - t_wait ) * 1e-9, (double)( t_end - t_start ) * 1e-9,   /* drain_s: catch-up + settle */
           ovrnp, ovrnr, pub, pub_before_halt, pub_sz, mismatch, false_pub, order_err, tpe, booted, err,
           lat.cnt, lat.cnt ? (double)lat.sum_ns / (double)lat.cnt * 1e-6 : -1., pct_ms( &lat, .5 ), pct_ms( &lat, .99 ),
-          pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6 );
+          pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6,
+          clk[2] ? .1 * (double)clk[1] / (double)clk[2] : 0., clk[5] ? .1 * (double)clk[4] / (double)clk[5] : 0.,
+          clk[8] ? .1 * (double)clk[7] / (double)clk[8] : 0., clk[0], clk[3], clk[6] );
   for( unsigned long k=0; k<FD_VERIFY_TILE_DIAG_CNT; k++ ) printf( "%s%lu", k ? ", " : "", d[k] );
   printf( "]}\n" );
 #ifdef FD_VT_PROF
