@@ -23,7 +23,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT, oracle_batch
-from live_common import expected_cyclic, read_pubout, run, write_frags
+from live_common import expected_cyclic, quiet_cpus, read_pubout, run, write_frags
 from test_verify_tile import expected_for, make_stream
 
 EXE = os.path.join(ROOT, "firedancer_amd", "vt_live")
@@ -35,12 +35,12 @@ def _exe():
 
 
 def _pin(n=2):
-    """producer and tile thread each on its own CPU of the GPU's NUMA node,
-    as the reference pins every tile to a core (fd_tile); unpinned, two
+    """producer and tile thread each on its own core of the GPU's NUMA node,
+    as the reference pins every tile to a core (fd_tile): the quietest
+    cores of a short sample (live_common.quiet_cpus); unpinned, two
     spinning threads that share a core stall each other for milliseconds"""
-    import firedancer_amd as fa
-    cpus = fa.numa_cpus(0) or sorted(os.sched_getaffinity(0))
-    return ",".join(str(c) for c in cpus[:n]) if len(cpus) >= n else None
+    c = quiet_cpus(n)
+    return {"cpus": c} if c else {}
 
 
 @pytest.mark.gpu
@@ -51,15 +51,16 @@ def test_task_live_producer_bounded_latency(ref, tmp_path, mode, rate, n_sigs):
     exp_pub, exp, nsig = expected_for(frags, ref)
     p, po = str(tmp_path / "frags.bin"), str(tmp_path / "pub.bin")
     write_frags(p, frags)
+    pin = _pin()
     t0 = os.times()
     d = run(_exe(), p, mode=mode, rate=rate, count=len(frags), depth=16384, batch=4096, eng_depth=8, pubout=po,
-            timeout=240, **({"cpus": _pin()} if _pin() else {}))
+            timeout=240, **pin)
     t1 = os.times()
     # this (parent) process's own CPU use while the harness ran: threads of
     # earlier tests still spinning here would compete with the harness
     parent = {"parent_cpu_s": round((t1.user - t0.user) + (t1.system - t0.system), 3),
               "wall_s": round(t1.elapsed - t0.elapsed, 3), "parent_threads": len(os.listdir("/proc/self/task")),
-              "pinned": _pin()}
+              "pinned": pin}
     assert d["rc"] == 0 and d["booted"] == 1 and d["err"] == 0, d
     # nothing overran: every frag was taken, in order
     assert d["taken"] == len(frags) and d["ovrnp"] == 0 and d["ovrnr"] == 0 and d["diag"]["OVRN_CNT"] == 0, d
@@ -116,6 +117,9 @@ def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
     assert free["rc"] == 0 and free["booted"] == 1, free
     assert free["mismatch"] == 0 and free["false_pub"] == 0 and free["order_err"] == 0, free
     assert free["pub"] <= free["taken_pass_expected"]
+    # exactly the reference's set of what the tile took, less the frags its
+    # overrun check dropped: nothing else lost, nothing flagged published
+    assert free["flagged"] > 0 and free["flag_pub"] == 0 and free["pub"] == free["pub_expected_exact"], free
     acc = sum(free["diag"][k] for k in ("PUB_CNT", "SV_FILT_CNT", "HA_FILT_CNT", "BAD_CNT", "OVRN_CNT"))
     assert acc == free["taken"], free
     print("free-running producer:", {k: free[k] for k in ("produced", "taken", "pub", "ovrnp", "ovrnr")},
@@ -144,11 +148,12 @@ def test_two_tiles_one_engine(ref, tmp_path, mode):
     ok.astype(np.uint8).tofile(ex)
     spf = np.mean([f[((int.from_bytes(f[-2:], "little") + 1) & ~1) + 1] for f in frags])
     d = run(_exe(), p, mode=mode, rate=10e6 / spf / 2, seconds=2, tiles=2, share=1, depth=16384, batch=4096,
-            eng_depth=8, expect=ex, timeout=240, **({"cpus": _pin(4)} if _pin(4) else {}))
+            eng_depth=8, expect=ex, timeout=240, **_pin(4))
     assert d["rc"] == 0 and d["booted"] == 1 and d["shared_engine"] == 1, d
     assert d["mismatch"] == 0 and d["false_pub"] == 0 and d["order_err"] == 0, d
     if d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0:
         assert d["pub"] == d["taken_pass_expected"], d
+    assert d["flag_pub"] == 0 and d["pub"] == d["pub_expected_exact"], d
     assert d["pub_before_halt"] == d["pub"]
     print(f"two tiles, one engine, {mode}: {d['taken_sigs_s'] / 1e6:.2f} M verifies/s, p50 {d['lat']['p50_ms']:.3f} "
           f"p99 {d['lat']['p99_ms']:.3f} max {d['lat']['max_ms']:.3f} ms")

@@ -96,7 +96,20 @@ struct live {
   unsigned long   pf;                   /* the input adapter prefetches frag want + pf */
   fd_verify_tile_lat_t * lat;
   FILE *          pubout;
+  /* the exact check under overruns: seqs taken and seqs the tile's ovrn
+     check flagged (bitmaps, task thread only); a tile publishes a taken
+     frag iff the reference does and its check never flagged it */
+  std::vector<unsigned long> taken_bm, flag_bm;
+  unsigned long   flag_pub;             /* publishes of a flagged seq */
 };
+
+static void bm_set( std::vector<unsigned long> & bm, unsigned long i ) {
+  if( (i >> 6) >= bm.size() ) bm.resize( ( (i >> 6) + (1UL << 20) ) & ~((1UL << 20) - 1UL), 0UL );
+  bm[ i >> 6 ] |= 1UL << (i & 63UL);
+}
+static int bm_get( std::vector<unsigned long> const & bm, unsigned long i ) {
+  return (i >> 6) < bm.size() && ((bm[ i >> 6 ] >> (i & 63UL)) & 1UL);
+}
 
 /* ---- producer ------------------------------------------------------------ */
 
@@ -178,6 +191,7 @@ static int in_seq( void * ctx, void const ** frag, unsigned long * sz, unsigned 
   }
   __builtin_prefetch( &L->mc[ (L->want + pf + 1UL) & L->mask ], 0, 3 );
   if( !L->expect().empty() && L->expect()[ L->want % L->n ] ) L->taken_pass_expected++;
+  bm_set( L->taken_bm, L->want );
   L->want++; L->taken++;
   L->want_a.store( L->want, std::memory_order_relaxed );
   L->taken_a.store( L->taken, std::memory_order_relaxed );
@@ -187,7 +201,9 @@ static int in_seq( void * ctx, void const ** frag, unsigned long * sz, unsigned 
 static int ovrn( void * ctx, unsigned long seq ) {
   live * L = (live *)ctx;
   std::atomic_thread_fence( std::memory_order_acquire );   /* the tile's reads of the frag come first */
-  return L->mc[ seq & L->mask ].seq.load( std::memory_order_acquire ) != seq;
+  int const o = L->mc[ seq & L->mask ].seq.load( std::memory_order_acquire ) != seq;
+  if( o ) bm_set( L->flag_bm, seq );
+  return o;
 }
 
 static void * chunk( void * ctx, unsigned long sz ) {
@@ -206,6 +222,7 @@ static void publish( void * ctx, unsigned long sig, void const * frag, unsigned 
   if( sz != f.size() || memcmp( frag, f.data(), sz ) ) L->mismatch++;
   if( !L->expect().empty() && !L->expect()[ seq % L->n ] ) L->false_pub++;
   if( L->any_pub && seq <= L->last_seq ) L->order_err++;
+  if( bm_get( L->flag_bm, seq ) ) L->flag_pub++;
   L->last_seq = seq; L->any_pub = 1;
   L->pub++; L->pub_sz += sz;
   L->pub_a.store( L->pub, std::memory_order_relaxed );
@@ -256,7 +273,13 @@ struct tile_run {
   int                   cpu_p, cpu_t;
 };
 
+static int rt_want;                     /* rt=1: the spinning threads ask for SCHED_FIFO */
+static std::atomic<int> rt_got;         /* threads that got it */
 static void pin( int cpu ) {
+  if( rt_want ) {
+    struct sched_param sp; memset( &sp, 0, sizeof(sp) ); sp.sched_priority = 1;
+    if( !sched_setscheduler( 0, SCHED_FIFO, &sp ) ) rt_got++;
+  }
   if( cpu < 0 ) return;
   cpu_set_t m; CPU_ZERO( &m ); CPU_SET( cpu, &m ); sched_setaffinity( 0, sizeof(m), &m );
 }
@@ -304,6 +327,7 @@ int main( int argc, char ** argv ) {
   char const *  cpus     = arg( argc, argv, "cpus", NULL );   /* "producer0,tile0,producer1,tile1,..." */
   int const     tiles    = atoi( arg( argc, argv, "tiles", "1" ) );   /* independent tiles on the device, one link each */
   int const     use_ovrn = atoi( arg( argc, argv, "ovrn", "1" ) );
+  rt_want = atoi( arg( argc, argv, "rt", "0" ) );
   if( tiles < 1 || tiles > 8 || (pubout && tiles > 1) ) { fprintf( stderr, "tiles: 1..8 (pubout: one tile)\n" ); return 2; }
 #ifdef VT_LIVE_FAKE
   fake_engine_cheap_default( atoi( arg( argc, argv, "cheap", "0" ) ) );
@@ -338,6 +362,11 @@ int main( int argc, char ** argv ) {
     L.out = (unsigned char *)malloc( L.out_sz );
     L.lat = (fd_verify_tile_lat_t *)calloc( 1, sizeof(fd_verify_tile_lat_t) );
     L.pubout = pubout ? fopen( pubout, "wb" ) : NULL;
+    {  /* the check bitmaps sized (and touched) up front: no growth on the tile thread */
+      double est = count ? (double)count : ( rate > 0. ? seconds * rate * 1.05 : 0. );
+      unsigned long words = ( (unsigned long)est >> 6 ) + (1UL << 14);
+      L.taken_bm.assign( words, 0UL ); L.flag_bm.assign( words, 0UL );
+    }
     L.fseq.store( 0 ); L.stop.store( 0 ); L.produced.store( 0 ); L.want_a.store( 0 ); L.pub_a.store( 0 ); L.taken_a.store( 0 );
     /* the task (init before any sandbox would close syscalls) */
     fd_verify_tile_args_t & a = tr->a;
@@ -430,7 +459,7 @@ int main( int argc, char ** argv ) {
   static fd_verify_tile_lat_t lat;
   memset( &lat, 0, sizeof(lat) );
   unsigned long produced = 0, taken = 0, ovrnp = 0, ovrnr = 0, pub = 0, pub_sz = 0, mismatch = 0, false_pub = 0, order_err = 0, tpe = 0;
-  unsigned long tp0 = ~0UL, tp1 = 0;
+  unsigned long tp0 = ~0UL, tp1 = 0, flag_pub = 0, pub_exact = 0, flagged = 0;
   for( int k=0; k<tiles; k++ ) {
     live & L = T[k]->L;
     for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ ) d[c] += T[k]->cnc.diag[c];
@@ -439,6 +468,17 @@ int main( int argc, char ** argv ) {
     for( unsigned long b=0; b<FD_VERIFY_TILE_LAT_BINS; b++ ) lat.bin[b] += L.lat->bin[b];
     produced += L.produced.load(); taken += L.taken; ovrnp += L.ovrnp; ovrnr += L.ovrnr; pub += L.pub; pub_sz += L.pub_sz;
     mismatch += L.mismatch; false_pub += L.false_pub; order_err += L.order_err; tpe += L.taken_pass_expected;
+    flag_pub += L.flag_pub;
+    /* what the reference publishes of what this tile took, less what its
+       overrun check dropped */
+    for( unsigned long w=0; w<L.taken_bm.size(); w++ ) {
+      unsigned long tb = L.taken_bm[w], fb = w < L.flag_bm.size() ? L.flag_bm[w] : 0UL;
+      flagged += (unsigned long)__builtin_popcountl( tb & fb );
+      for( unsigned long m = tb & ~fb; m; m &= m - 1UL ) {
+        unsigned long seq = (w << 6) + (unsigned long)__builtin_ctzl( m );
+        if( L.expect().empty() || L.expect()[ seq % L.n ] ) pub_exact++;
+      }
+    }
     if( L.t_prod0 < tp0 ) tp0 = L.t_prod0;
     if( L.t_prod1 > tp1 ) tp1 = L.t_prod1;
     err |= T[k]->a.err;
@@ -464,6 +504,7 @@ int main( int argc, char ** argv ) {
           "\"taken_sigs_s\": %.1f, \"published_frags_s\": %.1f, \"drain_s\": %.6f, \"run_s\": %.6f, "
           "\"ovrnp\": %lu, \"ovrnr\": %lu, \"pub\": %lu, \"pub_before_halt\": %lu, \"pub_sz\": %lu, "
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
+          "\"flagged\": %lu, \"flag_pub\": %lu, \"pub_expected_exact\": %lu, \"rt_threads\": %d, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
           "\"dsm_ghz\": {\"pool\": %.3f, \"quad\": %.3f, \"oct\": %.3f}, \"dsm_waves\": [%llu, %llu, %llu], "
           "\"diag\": [",
@@ -472,6 +513,7 @@ int main( int argc, char ** argv ) {
           el > 0. ? (double)d[ FD_VERIFY_TILE_DIAG_SIG_CNT ] / el : 0., el > 0. ? (double)pub / el : 0.,
           (double)( t_drain - t_wait ) * 1e-9, (double)( t_end - t_start ) * 1e-9,   /* drain_s: catch-up + settle */
           ovrnp, ovrnr, pub, pub_before_halt, pub_sz, mismatch, false_pub, order_err, tpe, booted, err,
+          flagged, flag_pub, pub_exact, rt_got.load(),
           lat.cnt, lat.cnt ? (double)lat.sum_ns / (double)lat.cnt * 1e-6 : -1., pct_ms( &lat, .5 ), pct_ms( &lat, .99 ),
           pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6,
           clk[2] ? .1 * (double)clk[1] / (double)clk[2] : 0., clk[5] ? .1 * (double)clk[4] / (double)clk[5] : 0.,

@@ -44,8 +44,8 @@ def main():
     tmp = tempfile.mkdtemp()
     fp, po = os.path.join(tmp, "frags.bin"), os.path.join(tmp, "pub.bin")
     write_frags(fp, frags)
-    cpus = fa.numa_cpus(0)
-    pin = ",".join(str(c) for c in cpus[:2]) if len(cpus) >= 2 else None
+    from live_common import quiet_cpus
+    pin = quiet_cpus(2)   # producer k, tile k: the quietest cores of the GPU's NUMA node
     for i in range(a.runs):
         for mode in a.modes.split(","):
             kw = dict(mode=mode, rate=a.rate, count=a.count, depth=16384, batch=4096, eng_depth=8, pubout=po,

@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--max-wait-ns", type=int, default=0)
     ap.add_argument("--tiles", type=int, default=1, help="verify tiles on the GPU, each with its own link and producer")
     ap.add_argument("--share", type=int, default=0, help="1: the tiles share one engine (fd_verify_tile_args_t.shared_gpu)")
+    ap.add_argument("--rt", type=int, default=0, help="1: the harness's spinning threads ask for SCHED_FIFO (reported as rt_threads)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -75,15 +76,15 @@ def main():
     fp, ex = os.path.join(tmp, "frags.bin"), os.path.join(tmp, "expect.bin")
     write_frags(fp, frags)
     ok.astype(np.uint8).tofile(ex)
-    cpus = fa.numa_cpus(0)
-    # producer k and tile k on distinct CPUs of the GPU's NUMA node
-    pin = ",".join(str(c) for c in cpus[:2 * a.tiles]) if len(cpus) >= 2 * a.tiles else None
+    from live_common import quiet_cpus
+    pin = quiet_cpus(2 * a.tiles)   # producer k, tile k: the quietest cores of the GPU's NUMA node
     exe = os.path.join(ROOT, "firedancer_amd", "vt_live")
     out = open(a.out, "a") if a.out else None
-    for mode in a.modes.split(","):
-        for r in [float(x) for x in a.rates.split(",")]:
+    # ',' or '+' between values ('+' survives tools/gpu.sh's py= step)
+    for mode in a.modes.replace("+", ",").split(","):
+        for r in [float(x) for x in a.rates.replace("+", ",").split(",")]:
             kw = dict(mode=mode, rate=r / spf / a.tiles, tiles=a.tiles, share=a.share, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
-                      eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex)
+                      eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex, rt=a.rt)
             if pin:
                 kw["cpus"] = pin
             t0 = time.time()
@@ -95,7 +96,12 @@ def main():
                       "reference_check": {"publishes_checked": d["pub"], "false_pub": d["false_pub"],
                                           "byte_mismatch": d["mismatch"], "order_err": d["order_err"],
                                           "pub_equals_reference_set": d["pub"] == d["taken_pass_expected"]
-                                          and d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0}})
+                                          and d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0,
+                                          # with overruns: the reference's set of the frags taken, less
+                                          # those the tile's overrun check dropped (tests/vt_live.cpp)
+                                          "overrun_dropped": d["flagged"], "flagged_published": d["flag_pub"],
+                                          "pub_equals_reference_set_less_overrun": d["pub"] == d["pub_expected_exact"]
+                                          and d["flag_pub"] == 0}})
             line = json.dumps(d)
             print(line, flush=True)
             if out:
