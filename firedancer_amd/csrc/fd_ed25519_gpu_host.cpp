@@ -57,6 +57,29 @@ static inline long fd_now_ns( void ) {
   return (long)t.tv_sec * 1000000000L + (long)t.tv_nsec;
 }
 
+/* The engine's ring lock.  Its callers are tiles, each spinning on a core
+   of its own, and on an engine shared by tiles (fd_verify_tile_args_t.
+   shared_gpu) two of them poll and submit through it every few
+   microseconds.  std::mutex parks a contended caller in the kernel at
+   once, and on a host with other work the woken thread can wait out
+   another task's time slice (milliseconds) before it runs again: spin on
+   try_lock for a while first (holders keep it for one HIP enqueue or
+   query, microseconds), then block. */
+struct fd_ring_lock {
+  std::mutex m;
+  void lock( void ) {
+    if( m.try_lock() ) return;
+    long const t0 = fd_now_ns();
+    do {
+      for( int i=0; i<16; i++ ) __builtin_ia32_pause();
+      if( m.try_lock() ) return;
+    } while( fd_now_ns() - t0 < 200000L );
+    m.lock();
+  }
+  bool try_lock( void ) { return m.try_lock(); }
+  void unlock( void ) { m.unlock(); }
+};
+
 /* Bounded wait on a completion query: spin (as a tile busy-polls its
    rings; a sleeping wake-up adds tens of microseconds to a ~0.8 ms batch
    round trip) for up to spin_ns, then query every ~50 us until timeout_ns
@@ -179,7 +202,7 @@ struct fd_ed25519_gpu {
   unsigned long dev_stats_cnt;
   hipEvent_t    dev_ev[FD_DEV_STATS_MAX][FD_EV_CNT];
   hipEvent_t    kev[FD_EV_CNT];   /* per-kernel timing events */
-  std::mutex    lock;
+  fd_ring_lock  lock;
 };
 
 static inline long fd_timeout( fd_ed25519_gpu_t const * g ) { return __atomic_load_n( &g->timeout_ns, __ATOMIC_RELAXED ); }
@@ -444,7 +467,7 @@ extern "C" int fd_ed25519_gpu_depth( fd_ed25519_gpu_t const * g ) { return g ? g
 static void fd_reclaim_orphans( fd_ed25519_gpu_t * g );
 extern "C" int fd_ed25519_gpu_set_cu_groups( fd_ed25519_gpu_t * g, int groups ) {
   if( !g || groups < 1 || groups > FD_GPU_DEPTH_MAX ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   /* a slot whose codes were taken early is idle for its caller: let it retire */
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].retiring && fd_event_wait( g->slot[s].done, fd_timeout( g ) ) ) return FD_ED25519_ERR_GPU;
   fd_reclaim_orphans( g );
@@ -461,7 +484,7 @@ extern "C" int fd_ed25519_gpu_cu_groups( fd_ed25519_gpu_t const * g ) { return g
    concurrently with a setter */
 struct fd_knobs { int mode; unsigned long pool_min, quad_max, oct_max; };
 static fd_knobs fd_knobs_get( fd_ed25519_gpu_t const * g ) {
-  std::lock_guard<std::mutex> guard( const_cast<fd_ed25519_gpu_t *>( g )->lock );
+  std::lock_guard<fd_ring_lock> guard( const_cast<fd_ed25519_gpu_t *>( g )->lock );
   fd_knobs k = { g->mode, g->pool_min, g->quad_max, g->oct_max };
   return k;
 }
@@ -502,7 +525,7 @@ static hipError_t fd_reg_release( void * host ) {
 
 extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsigned long sz ) {
   if( !g || !host || !sz ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   int k = 0;
   while( k<FD_REG_MAX && g->reg[k].p ) k++;
   if( k == FD_REG_MAX ) return FD_ED25519_ERR_ARG;
@@ -515,7 +538,7 @@ extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsig
 }
 extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) {
   if( !g || !host ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   for( int k=0; k<FD_REG_MAX; k++ ) if( g->reg[k].p == host ) {
     for( int s=0; s<g->depth; s++ ) {     /* no batch may still read from it */
       fd_ed25519_gpu_slot * sl = &g->slot[s];
@@ -536,7 +559,7 @@ static int fd_registered( fd_ed25519_gpu_t const * g, void const * p, unsigned l
 
 extern "C" int fd_ed25519_gpu_set_timeout( fd_ed25519_gpu_t * g, long timeout_ns ) {
   if( !g ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   __atomic_store_n( &g->timeout_ns, timeout_ns, __ATOMIC_RELAXED );
   return 0;
 }
@@ -544,28 +567,28 @@ extern "C" long fd_ed25519_gpu_timeout( fd_ed25519_gpu_t const * g ) { return g 
 
 extern "C" int fd_ed25519_gpu_set_mode( fd_ed25519_gpu_t * g, int mode ) {
   if( !g || (mode != FD_ED25519_GPU_MODE_AVX && mode != FD_ED25519_GPU_MODE_PORTABLE && mode != FD_ED25519_GPU_MODE_STRICT) ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   g->mode = mode;
   return 0;
 }
 extern "C" int fd_ed25519_gpu_mode( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).mode : -1; }
 extern "C" int fd_ed25519_gpu_set_dsm_pool_min( fd_ed25519_gpu_t * g, unsigned long n ) {
   if( !g ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   g->pool_min = n;
   return 0;
 }
 extern "C" unsigned long fd_ed25519_gpu_dsm_pool_min( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).pool_min : 0UL; }
 extern "C" int fd_ed25519_gpu_set_dsm_quad_max( fd_ed25519_gpu_t * g, unsigned long n ) {
   if( !g ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   g->quad_max = n;
   return 0;
 }
 extern "C" unsigned long fd_ed25519_gpu_dsm_quad_max( fd_ed25519_gpu_t const * g ) { return g ? fd_knobs_get( g ).quad_max : 0UL; }
 extern "C" int fd_ed25519_gpu_set_dsm_oct_max( fd_ed25519_gpu_t * g, unsigned long n ) {
   if( !g ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   g->oct_max = n;
   return 0;
 }
@@ -592,7 +615,7 @@ static void fd_reclaim_orphans( fd_ed25519_gpu_t * g ) {
    timed out): the slot is reclaimed by fd_reclaim_orphans once the batch
    drains, instead of staying taken for the engine's lifetime. */
 static void fd_abandon_ticket( fd_ed25519_gpu_t * g, unsigned long ticket ) {
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].ticket == ticket ) g->slot[s].orphan = 1;
 }
 
@@ -620,7 +643,7 @@ static int fd_wait_retiring( fd_ed25519_gpu_t * g ) {
 /* Lend a free slot's pinned staging buffers (zero-copy submit). */
 extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25519_gpu_desc_t ** desc ) {
   if( !g || !blob || !desc ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   fd_reclaim_orphans( g );
   for( int pass=0; pass<2; pass++ ) {
     for( int s=0; s<g->depth; s++ ) {
@@ -639,7 +662,7 @@ extern "C" int fd_ed25519_gpu_stage( fd_ed25519_gpu_t * g, void ** blob, fd_ed25
    holds it -- ADVICE r05). */
 extern "C" void fd_ed25519_gpu_unstage( fd_ed25519_gpu_t * g, void const * blob ) {
   if( !g ) return;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) g->slot[s].staged = 0;
 }
 
@@ -926,7 +949,7 @@ extern "C" int fd_ed25519_gpu_verify_packed( fd_ed25519_gpu_t * g, unsigned long
                                              fd_ed25519_gpu_desc_t const * desc, int * out ) {
   if( !g || n > g->max_sigs || blob_sz > g->max_blob || (n && (!desc || !out)) || (blob_sz && !blob) ) return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   /* use a free slot; synchronous callers serialise on the lock */
@@ -948,7 +971,7 @@ extern "C" int fd_ed25519_gpu_try_submit2( fd_ed25519_gpu_t * g, unsigned long n
                                            fd_ed25519_gpu_desc_t const * desc, unsigned long * ticket ) {
   if( !g || !ticket || n > g->max_sigs || blob_sz > g->max_blob || blob2_sz > g->max_blob - blob_sz || (n && !desc)
       || (blob_sz && !blob) || (blob2_sz && !blob2) ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
@@ -994,7 +1017,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
   if( !g || !ticket ) return FD_ED25519_ERR_ARG;
   fd_ed25519_gpu_slot * sl = NULL;
   {
-    std::lock_guard<std::mutex> guard( g->lock );
+    std::lock_guard<fd_ring_lock> guard( g->lock );
     for( int s=0; s<g->depth && !sl; s++ ) if( g->slot[s].ticket == ticket ) sl = &g->slot[s];
   }
   if( !sl ) return FD_ED25519_ERR_ARG;
@@ -1008,7 +1031,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     }
     if( r == 1 ) {
       /* the codes are in; the slot comes back once its event completes */
-      std::lock_guard<std::mutex> guard( g->lock );
+      std::lock_guard<fd_ring_lock> guard( g->lock );
       if( out ) fd_slot_collect( sl, out );
       sl->early = 0; sl->retiring = 1;
       if( block & FD_ED25519_GPU_POLL_KEEP ) sl->staged = 1;   /* its pinned buffers stay the caller's */
@@ -1022,7 +1045,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
     if( e == hipErrorNotReady ) return 0;
     if( e != hipSuccess ) return fd_gpu_fail( "poll", e );
   }
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   if( out ) fd_slot_collect( sl, out );
   sl->ticket = 0; sl->early = 0;
   if( block & FD_ED25519_GPU_POLL_KEEP ) sl->staged = 1;   /* lent back to the caller (unstage to free) */
@@ -1036,7 +1059,7 @@ extern "C" int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * g, unsigned long ticket, 
 extern "C" int fd_ed25519_gpu_debug_fe( fd_ed25519_gpu_t * g, int op, unsigned long n, int const * f, int const * gg, int * h ) {
   if( !g || op < 0 || op > 7 || n > (1UL<<20) || (n && (!f || !gg || !h)) ) return FD_ED25519_ERR_ARG;
   if( !n ) return 0;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
@@ -1076,7 +1099,7 @@ extern "C" int fd_ed25519_gpu_debug_k( fd_ed25519_gpu_t * g, unsigned long n, vo
      holding it: their knobs are read before), so no two threads can wait
      on each other's lock */
   std::lock_guard<std::mutex> dguard( g->dev_lock );
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, NULL );
@@ -1121,7 +1144,7 @@ extern "C" int fd_ed25519_gpu_sha512_packed( fd_ed25519_gpu_t * g, unsigned long
   if( !n ) return 0;
   for( unsigned long i=0; i<n; i++ )
     if( (unsigned long)desc[i].msg_off + (unsigned long)desc[i].msg_sz > blob_sz ) return FD_ED25519_ERR_ARG;
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   hipError_t e = hipSetDevice( g->device );
   if( e != hipSuccess ) return fd_gpu_fail( "hipSetDevice", e );
   fd_ed25519_gpu_slot * sl = fd_free_slot( g, blob );
@@ -1261,7 +1284,7 @@ static void fd_long_pack( uint8_t * dst, fd_long_req const & r, unsigned long po
 
 /* the staged slot owning blob (the caller holds the stage) */
 static fd_ed25519_gpu_slot * fd_slot_of( fd_ed25519_gpu_t * g, void const * blob ) {
-  std::lock_guard<std::mutex> guard( g->lock );
+  std::lock_guard<fd_ring_lock> guard( g->lock );
   for( int s=0; s<g->depth; s++ ) if( g->slot[s].h_blob == blob ) return &g->slot[s];
   return NULL;
 }
@@ -1273,7 +1296,7 @@ static int fd_long_wait( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl ) {
   if( e != hipSuccess ) return fd_gpu_fail( "long: event", e );
   int err = fd_event_wait( sl->done, fd_timeout( g ) );
   if( err ) {
-    std::lock_guard<std::mutex> guard( g->lock );
+    std::lock_guard<fd_ring_lock> guard( g->lock );
     sl->ticket = g->next_ticket++; sl->orphan = 1; sl->staged = 0;
   }
   return err;

@@ -322,7 +322,7 @@ static int fd_vt_wait_any( fd_verify_tile_t * t ) {
     if( fd_vt_pick_engine( t ) >= 0 ) return 0;   /* an engine finished a batch: it is below its cap */
     unsigned long dt = fd_vt_now() - t0;
     if( to >= 0 && dt > (unsigned long)to ) return FD_ED25519_ERR_GPU;
-    if( dt < 200000UL ) _mm_pause();
+    if( dt < 20000000UL ) _mm_pause();     /* spin, as fd_vt_wait_slot */
     else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
   }
 }
@@ -339,8 +339,13 @@ static int fd_vt_wait_slot( fd_verify_tile_t * t, TRY try_ ) {
   for(;;) {
     int r = try_();
     if( r ) return r;
-    if( to >= 0 && fd_vt_now() - t0 > (unsigned long)to ) return FD_ED25519_ERR_GPU;
-    struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL );
+    unsigned long dt = fd_vt_now() - t0;
+    if( to >= 0 && dt > (unsigned long)to ) return FD_ED25519_ERR_GPU;
+    /* a tile owns its core: spin (a sleep hands the core to other work,
+       which on a busy host keeps it for milliseconds), sleeping only once
+       the wait is already long */
+    if( dt < 20000000UL ) _mm_pause();
+    else { struct timespec ts = { 0, 20000L }; nanosleep( &ts, NULL ); }
   }
 }
 

@@ -91,7 +91,13 @@ def read_pubout(path):
 def run(exe, frags_path, timeout=300, env=None, **kw):
     """run the harness; returns its JSON line as a dict (+ rc, stderr tail)"""
     args = [exe, frags_path] + [f"{k}={v}" for k, v in kw.items()]
-    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
+    try:
+        r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:      # killed at the limit: say where it was
+        def txt(x):
+            return x.decode(errors="replace") if isinstance(x, bytes) else (x or "")
+        raise AssertionError(f"harness timed out after {timeout} s: {args[2:]}\nstdout: {txt(e.stdout)[-2000:]}"
+                             f"\nstderr: {txt(e.stderr)[-4000:]}") from None
     lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
     assert lines, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     d = json.loads(lines[-1])

@@ -42,6 +42,8 @@
 #include <string.h>
 #include <time.h>
 #include <sched.h>
+#include <sys/resource.h>
+#include <x86intrin.h>
 #include <atomic>
 #include <thread>
 #include <vector>
@@ -101,6 +103,12 @@ struct live {
      frag iff the reference does and its check never flagged it */
   std::vector<unsigned long> taken_bm, flag_bm;
   unsigned long   flag_pub;             /* publishes of a flagged seq */
+  /* the tile thread's own view of stalls: the longest gap between two
+     calls of its input callback (TSC ticks; the run loop calls it every
+     pass) and its context switches over the run (getrusage RUSAGE_THREAD:
+     involuntary ones on a pinned core are other work preempting it) */
+  unsigned long   last_tsc, max_gap_tsc;
+  long            nvcsw, nivcsw;
 };
 
 static void bm_set( std::vector<unsigned long> & bm, unsigned long i ) {
@@ -158,6 +166,11 @@ static void producer( live * L ) {
 static int in_seq( void * ctx, void const ** frag, unsigned long * sz, unsigned long * ctl, unsigned long * tsorig,
                    unsigned long * seq ) {
   live * L = (live *)ctx;
+  {
+    unsigned long const tsc = __rdtsc();
+    if( L->last_tsc && tsc - L->last_tsc > L->max_gap_tsc && L->want >= L->warm ) L->max_gap_tsc = tsc - L->last_tsc;
+    L->last_tsc = tsc;
+  }
   if( L->credit ) {
     unsigned long rel = L->inplace ? fd_verify_tile_held( L->args->tile ) : L->want;
     L->fseq.store( rel, std::memory_order_release );
@@ -399,11 +412,35 @@ int main( int argc, char ** argv ) {
 #endif
   unsigned long t_start = now_ns();
   std::vector<std::thread> runs, prods;
-  for( int k=0; k<tiles; k++ ) runs.emplace_back( [&, k]() { pin( T[k]->cpu_t ); task->run( &T[k]->a ); } );
+  /* a monitor: every 5 s, to stderr, where main is and each tile's link
+     and cnc state (a run that outlives its time limit then says where) */
+  static std::atomic<int> phase( 1 ), mon_stop( 0 );
+  std::thread mon( [&]() {
+    unsigned long const t0 = now_ns();
+    while( !mon_stop.load() ) {
+      for( int i=0; i<50 && !mon_stop.load(); i++ ) { struct timespec t = { 0, 100000000L }; nanosleep( &t, NULL ); }
+      if( mon_stop.load() ) break;
+      fprintf( stderr, "vt_live t=%.1fs phase=%d", (double)( now_ns() - t0 ) * 1e-9, phase.load() );
+      for( int k=0; k<tiles; k++ )
+        fprintf( stderr, " | tile %d produced=%lu want=%lu taken=%lu pub=%lu signal=%lu", k, T[k]->L.produced.load(),
+                 T[k]->L.want_a.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load(), sig_load( &T[k]->cnc ) );
+      fprintf( stderr, "\n" );
+    }
+  } );
+  unsigned long const tsc0 = __rdtsc();
+  for( int k=0; k<tiles; k++ ) runs.emplace_back( [&, k]() {
+    pin( T[k]->cpu_t );
+    struct rusage r0, r1;
+    getrusage( RUSAGE_THREAD, &r0 );
+    task->run( &T[k]->a );
+    getrusage( RUSAGE_THREAD, &r1 );
+    T[k]->L.nvcsw = r1.ru_nvcsw - r0.ru_nvcsw; T[k]->L.nivcsw = r1.ru_nivcsw - r0.ru_nivcsw;
+  } );
   int ok = 1;
   for( int k=0; k<tiles; k++ ) ok &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_RUN, 30. );
   for( int k=0; k<tiles; k++ ) prods.emplace_back( [&, k]() { pin( T[k]->cpu_p ); if( ok ) producer( &T[k]->L ); } );
   for( auto & th : prods ) th.join();
+  phase.store( 2 );   /* catching up */
   /* let each consumer catch up with its producer (bounded), then wait
      (bounded: settle_s) until the run loop has accounted for every frag
      it took -- published, filtered or dropped, per the diagnostics it
@@ -422,6 +459,7 @@ int main( int argc, char ** argv ) {
     }
   }
   unsigned long t_drain = now_ns();
+  phase.store( 3 );   /* settling */
   for( int k=0; k<tiles; k++ ) {
     for(;;) {
       unsigned long acc = 0;
@@ -451,15 +489,19 @@ int main( int argc, char ** argv ) {
   if( shared || tiles == 1 ) fd_ed25519_gpu_dsm_clock( shared ? shared : T[0]->a.gpu, 0, clk );
 #endif
   for( int k=0; k<tiles; k++ ) T[k]->L.stop.store( 1 );
+  phase.store( 4 );   /* halted, joining the tasks */
   for( auto & th : runs ) th.join();
+  phase.store( 5 );   /* reporting */
   unsigned long t_end = now_ns();
+  double const tsc_per_ns = (double)( __rdtsc() - tsc0 ) / (double)( t_end - t_start );
 
   /* the tiles summed */
   unsigned long d[ FD_VERIFY_TILE_DIAG_CNT ] = { 0 };
   static fd_verify_tile_lat_t lat;
   memset( &lat, 0, sizeof(lat) );
   unsigned long produced = 0, taken = 0, ovrnp = 0, ovrnr = 0, pub = 0, pub_sz = 0, mismatch = 0, false_pub = 0, order_err = 0, tpe = 0;
-  unsigned long tp0 = ~0UL, tp1 = 0, flag_pub = 0, pub_exact = 0, flagged = 0;
+  unsigned long tp0 = ~0UL, tp1 = 0, flag_pub = 0, pub_exact = 0, flagged = 0, max_gap = 0;
+  long nvcsw = 0, nivcsw = 0;
   for( int k=0; k<tiles; k++ ) {
     live & L = T[k]->L;
     for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ ) d[c] += T[k]->cnc.diag[c];
@@ -469,6 +511,8 @@ int main( int argc, char ** argv ) {
     produced += L.produced.load(); taken += L.taken; ovrnp += L.ovrnp; ovrnr += L.ovrnr; pub += L.pub; pub_sz += L.pub_sz;
     mismatch += L.mismatch; false_pub += L.false_pub; order_err += L.order_err; tpe += L.taken_pass_expected;
     flag_pub += L.flag_pub;
+    if( L.max_gap_tsc > max_gap ) max_gap = L.max_gap_tsc;
+    nvcsw += L.nvcsw; nivcsw += L.nivcsw;
     /* what the reference publishes of what this tile took, less what its
        overrun check dropped */
     for( unsigned long w=0; w<L.taken_bm.size(); w++ ) {
@@ -505,6 +549,7 @@ int main( int argc, char ** argv ) {
           "\"ovrnp\": %lu, \"ovrnr\": %lu, \"pub\": %lu, \"pub_before_halt\": %lu, \"pub_sz\": %lu, "
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
           "\"flagged\": %lu, \"flag_pub\": %lu, \"pub_expected_exact\": %lu, \"rt_threads\": %d, "
+          "\"tile_max_gap_ms\": %.4f, \"tile_nvcsw\": %ld, \"tile_nivcsw\": %ld, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
           "\"dsm_ghz\": {\"pool\": %.3f, \"quad\": %.3f, \"oct\": %.3f}, \"dsm_waves\": [%llu, %llu, %llu], "
           "\"diag\": [",
@@ -514,6 +559,7 @@ int main( int argc, char ** argv ) {
           (double)( t_drain - t_wait ) * 1e-9, (double)( t_end - t_start ) * 1e-9,   /* drain_s: catch-up + settle */
           ovrnp, ovrnr, pub, pub_before_halt, pub_sz, mismatch, false_pub, order_err, tpe, booted, err,
           flagged, flag_pub, pub_exact, rt_got.load(),
+          (double)max_gap / tsc_per_ns * 1e-6, nvcsw, nivcsw,
           lat.cnt, lat.cnt ? (double)lat.sum_ns / (double)lat.cnt * 1e-6 : -1., pct_ms( &lat, .5 ), pct_ms( &lat, .99 ),
           pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6,
           clk[2] ? .1 * (double)clk[1] / (double)clk[2] : 0., clk[5] ? .1 * (double)clk[4] / (double)clk[5] : 0.,
@@ -530,6 +576,7 @@ int main( int argc, char ** argv ) {
   }
 #endif
   fflush( stdout );
+  phase.store( 6 );   /* fini */
   for( int k=0; k<tiles; k++ ) {
     task->fini( &T[k]->a );
     if( k == tiles - 1 && shared ) fd_ed25519_gpu_delete( shared );
@@ -537,5 +584,7 @@ int main( int argc, char ** argv ) {
     delete [] L.mc; free( L.dc ); free( L.out ); free( L.lat );
     delete T[k];
   }
+  mon_stop.store( 1 );
+  mon.join();
   return booted && !err ? 0 : 1;
 }
