@@ -44,6 +44,9 @@
 #include <sched.h>
 #include <sys/resource.h>
 #include <x86intrin.h>
+#include <unistd.h>
+#include <sys/syscall.h>
+#include <map>
 #include <atomic>
 #include <thread>
 #include <vector>
@@ -109,6 +112,7 @@ struct live {
      involuntary ones on a pinned core are other work preempting it) */
   unsigned long   last_tsc, max_gap_tsc;
   long            nvcsw, nivcsw;
+  std::atomic<long> tid;                /* the tile thread's kernel id (sample=1) */
 };
 
 static void bm_set( std::vector<unsigned long> & bm, unsigned long i ) {
@@ -427,9 +431,33 @@ int main( int argc, char ** argv ) {
       fprintf( stderr, "\n" );
     }
   } );
+  /* sample=1: a poor man's profiler of where tile 0's thread waits --
+     every ~200 us read /proc/self/task/TID/syscall (the syscall it is
+     blocked in, or "running") and count */
+  std::map<std::string, unsigned long> samp;
+  int const do_samp = atoi( arg( argc, argv, "sample", "0" ) );
+  std::thread sampler;
+  if( do_samp ) sampler = std::thread( [&]() {
+    while( !T[0]->L.tid.load() && !mon_stop.load() ) { struct timespec t = { 0, 100000L }; nanosleep( &t, NULL ); }
+    char path[64]; snprintf( path, sizeof(path), "/proc/self/task/%ld/syscall", T[0]->L.tid.load() );
+    while( phase.load() < 4 ) {
+      FILE * f = fopen( path, "r" );
+      if( f ) {
+        char buf[256] = { 0 };
+        if( fgets( buf, sizeof(buf), f ) ) {
+          char * sp = strchr( buf, ' ' ); if( sp ) *sp = 0;
+          char * nl = strchr( buf, '\n' ); if( nl ) *nl = 0;
+          samp[ buf ]++;
+        }
+        fclose( f );
+      }
+      struct timespec t = { 0, 200000L }; nanosleep( &t, NULL );
+    }
+  } );
   unsigned long const tsc0 = __rdtsc();
   for( int k=0; k<tiles; k++ ) runs.emplace_back( [&, k]() {
     pin( T[k]->cpu_t );
+    T[k]->L.tid.store( (long)syscall( SYS_gettid ) );
     struct rusage r0, r1;
     getrusage( RUSAGE_THREAD, &r0 );
     task->run( &T[k]->a );
@@ -490,6 +518,7 @@ int main( int argc, char ** argv ) {
 #endif
   for( int k=0; k<tiles; k++ ) T[k]->L.stop.store( 1 );
   phase.store( 4 );   /* halted, joining the tasks */
+  if( sampler.joinable() ) sampler.join();
   for( auto & th : runs ) th.join();
   phase.store( 5 );   /* reporting */
   unsigned long t_end = now_ns();
@@ -565,7 +594,14 @@ int main( int argc, char ** argv ) {
           clk[2] ? .1 * (double)clk[1] / (double)clk[2] : 0., clk[5] ? .1 * (double)clk[4] / (double)clk[5] : 0.,
           clk[8] ? .1 * (double)clk[7] / (double)clk[8] : 0., clk[0], clk[3], clk[6] );
   for( unsigned long k=0; k<FD_VERIFY_TILE_DIAG_CNT; k++ ) printf( "%s%lu", k ? ", " : "", d[k] );
-  printf( "]}\n" );
+  printf( "]" );
+  if( do_samp ) {
+    printf( ", \"tile0_syscall_samples\": {" );
+    int first = 1;
+    for( auto const & kv : samp ) { printf( "%s\"%s\": %lu", first ? "" : ", ", kv.first.c_str(), kv.second ); first = 0; }
+    printf( "}" );
+  }
+  printf( "}\n" );
 #ifdef FD_VT_PROF
   {  /* profiling builds: the tile's per-phase TSC cycles (fd_verify_tile.cpp FD_VT_PROF) */
     extern unsigned long fd_vt_prof[8];

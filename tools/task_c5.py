@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--tiles", type=int, default=1, help="verify tiles on the GPU, each with its own link and producer")
     ap.add_argument("--share", type=int, default=0, help="1: the tiles share one engine (fd_verify_tile_args_t.shared_gpu)")
     ap.add_argument("--rt", type=int, default=0, help="1: the harness's spinning threads ask for SCHED_FIFO (reported as rt_threads)")
+    ap.add_argument("--sample", type=int, default=0, help="1: sample where tile 0's thread waits (tile0_syscall_samples)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -84,7 +85,7 @@ def main():
     for mode in a.modes.replace("+", ",").split(","):
         for r in [float(x) for x in a.rates.replace("+", ",").split(",")]:
             kw = dict(mode=mode, rate=r / spf / a.tiles, tiles=a.tiles, share=a.share, seconds=a.seconds, warm=a.warm, depth=a.depth, batch=a.batch,
-                      eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex, rt=a.rt)
+                      eng_depth=a.eng_depth, max_wait_ns=a.max_wait_ns, expect=ex, rt=a.rt, sample=a.sample)
             if pin:
                 kw["cpus"] = pin
             t0 = time.time()
