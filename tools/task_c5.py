@@ -90,6 +90,9 @@ def main():
                 kw["cpus"] = pin
             t0 = time.time()
             d = run(exe, fp, timeout=a.seconds + 120, **kw)
+            if "error" in d:      # the harness refused the configuration (e.g. an engine depth past the maximum)
+                print(json.dumps({"error": d["error"], "config": kw, "rc": d["rc"]}), flush=True)
+                continue
             d.pop("stderr", None)
             d.update({"offered_verifies_s": r, "sigs_per_frag": spf, "corpus_frags": len(frags),
                       "corpus_reference_pass": int(ok.sum()), "cpus": pin, "wall_s": time.time() - t0,
