@@ -111,6 +111,13 @@ struct live {
      pass) and its context switches over the run (getrusage RUSAGE_THREAD:
      involuntary ones on a pinned core are other work preempting it) */
   unsigned long   last_tsc, max_gap_tsc;
+  /* where the tile thread's time goes, by the input callback's view (TSC):
+     inside the callback (a frag / nothing), and from its return to the
+     next call after a frag (rx: parse, dedup, copy or span, submits, and
+     every 8th frag a housekeeping pass) or after nothing (the idle
+     service: polls, publishes, wait-bound submits) */
+  unsigned long   t_exit, cy_in_got, cy_in_idle, cy_after_got, cy_after_idle, n_got, n_idle;
+  int             last_got;
   long            nvcsw, nivcsw;
   std::atomic<long> tid;                /* the tile thread's kernel id (sample=1) */
 };
@@ -167,14 +174,25 @@ static void producer( live * L ) {
 
 /* ---- consumer: the task's input (in_seq), overrun check, publish chunk ---- */
 
+static int in_seq_body( live * L, void const ** frag, unsigned long * sz, unsigned long * ctl, unsigned long * tsorig,
+                        unsigned long * seq );
+
 static int in_seq( void * ctx, void const ** frag, unsigned long * sz, unsigned long * ctl, unsigned long * tsorig,
                    unsigned long * seq ) {
   live * L = (live *)ctx;
-  {
-    unsigned long const tsc = __rdtsc();
-    if( L->last_tsc && tsc - L->last_tsc > L->max_gap_tsc && L->want >= L->warm ) L->max_gap_tsc = tsc - L->last_tsc;
-    L->last_tsc = tsc;
-  }
+  unsigned long const tsc = __rdtsc();
+  if( L->last_tsc && tsc - L->last_tsc > L->max_gap_tsc && L->want >= L->warm ) L->max_gap_tsc = tsc - L->last_tsc;
+  L->last_tsc = tsc;
+  if( L->t_exit ) { if( L->last_got ) L->cy_after_got += tsc - L->t_exit; else L->cy_after_idle += tsc - L->t_exit; }
+  int const got = in_seq_body( L, frag, sz, ctl, tsorig, seq );
+  L->t_exit = __rdtsc();
+  if( got ) { L->cy_in_got += L->t_exit - tsc; L->n_got++; } else { L->cy_in_idle += L->t_exit - tsc; L->n_idle++; }
+  L->last_got = got;
+  return got;
+}
+
+static int in_seq_body( live * L, void const ** frag, unsigned long * sz, unsigned long * ctl, unsigned long * tsorig,
+                        unsigned long * seq ) {
   if( L->credit ) {
     unsigned long rel = L->inplace ? fd_verify_tile_held( L->args->tile ) : L->want;
     L->fseq.store( rel, std::memory_order_release );
@@ -531,6 +549,7 @@ int main( int argc, char ** argv ) {
   unsigned long produced = 0, taken = 0, ovrnp = 0, ovrnr = 0, pub = 0, pub_sz = 0, mismatch = 0, false_pub = 0, order_err = 0, tpe = 0;
   unsigned long tp0 = ~0UL, tp1 = 0, flag_pub = 0, pub_exact = 0, flagged = 0, max_gap = 0;
   long nvcsw = 0, nivcsw = 0;
+  unsigned long cy[4] = { 0 }, n_got = 0, n_idle = 0;
   for( int k=0; k<tiles; k++ ) {
     live & L = T[k]->L;
     for( unsigned long c=0; c<FD_VERIFY_TILE_DIAG_CNT; c++ ) d[c] += T[k]->cnc.diag[c];
@@ -542,6 +561,8 @@ int main( int argc, char ** argv ) {
     flag_pub += L.flag_pub;
     if( L.max_gap_tsc > max_gap ) max_gap = L.max_gap_tsc;
     nvcsw += L.nvcsw; nivcsw += L.nivcsw;
+    cy[0] += L.cy_in_got; cy[1] += L.cy_after_got; cy[2] += L.cy_in_idle; cy[3] += L.cy_after_idle;
+    n_got += L.n_got; n_idle += L.n_idle;
     /* what the reference publishes of what this tile took, less what its
        overrun check dropped */
     for( unsigned long w=0; w<L.taken_bm.size(); w++ ) {
@@ -579,6 +600,7 @@ int main( int argc, char ** argv ) {
           "\"mismatch\": %lu, \"false_pub\": %lu, \"order_err\": %lu, \"taken_pass_expected\": %lu, \"booted\": %d, \"err\": %d, "
           "\"flagged\": %lu, \"flag_pub\": %lu, \"pub_expected_exact\": %lu, \"rt_threads\": %d, "
           "\"tile_max_gap_ms\": %.4f, \"tile_nvcsw\": %ld, \"tile_nivcsw\": %ld, "
+          "\"tile_ns\": {\"per_frag_in\": %.1f, \"per_frag_after\": %.1f, \"idle_frac\": %.4f, \"idle_polls\": %lu}, "
           "\"lat\": {\"count\": %lu, \"mean_ms\": %.4f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"p999_ms\": %.4f, \"max_ms\": %.4f}, "
           "\"dsm_ghz\": {\"pool\": %.3f, \"quad\": %.3f, \"oct\": %.3f}, \"dsm_waves\": [%llu, %llu, %llu], "
           "\"diag\": [",
@@ -589,6 +611,8 @@ int main( int argc, char ** argv ) {
           ovrnp, ovrnr, pub, pub_before_halt, pub_sz, mismatch, false_pub, order_err, tpe, booted, err,
           flagged, flag_pub, pub_exact, rt_got.load(),
           (double)max_gap / tsc_per_ns * 1e-6, nvcsw, nivcsw,
+          n_got ? (double)cy[0] / tsc_per_ns / (double)n_got : 0., n_got ? (double)cy[1] / tsc_per_ns / (double)n_got : 0.,
+          ( cy[0] + cy[1] + cy[2] + cy[3] ) ? (double)( cy[2] + cy[3] ) / (double)( cy[0] + cy[1] + cy[2] + cy[3] ) : 0., n_idle,
           lat.cnt, lat.cnt ? (double)lat.sum_ns / (double)lat.cnt * 1e-6 : -1., pct_ms( &lat, .5 ), pct_ms( &lat, .99 ),
           pct_ms( &lat, .999 ), (double)lat.max_ns * 1e-6,
           clk[2] ? .1 * (double)clk[1] / (double)clk[2] : 0., clk[5] ? .1 * (double)clk[4] / (double)clk[5] : 0.,
