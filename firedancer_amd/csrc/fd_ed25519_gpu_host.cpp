@@ -873,7 +873,10 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
      descriptors packed after it (one copy) */
   int direct = sl->h_blob != blob && sz0 && fd_registered( g, blob, sz0 )
             && ( !blob2_sz || fd_registered( g, blob2, blob2_sz ) );
-  if( direct ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  /* descriptors in a registered region too go from where they lie (a
+     verify tile building batches in its own registered buffers) */
+  int const ddirect = direct && fd_registered( g, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  if( direct && !ddirect ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   else {
     if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, sz0 );
     if( blob2_sz ) memcpy( sl->h_blob + sz0, blob2, blob2_sz );
@@ -893,7 +896,8 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
       return fd_gpu_fail( "H2D blob (registered)", e );
     if( blob2_sz && (e = hipMemcpyAsync( sl->d_blob + sz0, blob2, blob2_sz, hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D blob piece 2 (registered)", e );
-    if( (e = hipMemcpyAsync( sl->d_blob + doff, sl->h_desc, n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
+    if( (e = hipMemcpyAsync( sl->d_blob + doff, ddirect ? (void const *)desc : (void const *)sl->h_desc,
+                             n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D desc", e );
   } else if( (e = hipMemcpyAsync( sl->d_blob, sl->h_blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
     return fd_gpu_fail( "H2D blob+desc", e );

@@ -178,6 +178,13 @@ struct fd_verify_tile {
   fd_verify_tile_chunk_fn   chunk;
   void *                    octx;
   std::vector<uint8_t>      bounce;       /* in place, no chunk callback: the publish copy */
+  /* copy mode with own buffers (fd_verify_tile_new): batches are built in
+     depth + 2 buffers of the tile's own (region / region_sz / all above),
+     registered with the engine, and submitted like in-place spans -- a
+     batch takes a ring slot only from its close to its poll, not while it
+     fills or waits for its in-order publish.  0: the engine's staged
+     slots (registration failed, or $FD_VERIFY_TILE_COPY_STAGED=1) */
+  int                       own;
 };
 
 /* A frag into the open batch with streaming (non-temporal) stores: the
@@ -230,7 +237,7 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
     /* copy mode publishes from the slot's pinned blob: keep it lent until
        the publishes are done (an engine shared with other tiles would
        otherwise hand the slot to one of them now) */
-    int const keep = t->inplace ? 0 : FD_ED25519_GPU_POLL_KEEP;
+    int const keep = ( t->inplace || t->own ) ? 0 : FD_ED25519_GPU_POLL_KEEP;
     int r = fd_ed25519_gpu_poll( t->gpu, b->ticket, t->out.data(), (block ? 1 : 0) | keep );
     if( r <= 0 ) return r ? FD_ED25519_ERR_GPU : 0;
     codes = t->out.data();
@@ -271,7 +278,7 @@ static int fd_vt_complete( fd_verify_tile_t * t, fd_vt_batch * b, int block ) {
 #ifdef FD_VT_PROF
   fd_vt_prof[7]++;
 #endif
-  if( !t->multi && !t->inplace ) fd_ed25519_gpu_unstage( t->gpu, b->blob );   /* the slot's blob back to the engine */
+  if( !t->multi && !t->inplace && !t->own ) fd_ed25519_gpu_unstage( t->gpu, b->blob );   /* the slot's blob back to the engine */
   b->txns.clear(); b->ticket = 0;
   t->pool.push_back( b );
   return 1;
@@ -353,7 +360,7 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
   fd_vt_batch * b = t->open;
   if( !b || !b->nsig ) return 0;
   _mm_sfence();   /* the batch's streaming stores are visible before the device is told */
-  if( t->inplace && !t->multi ) {
+  if( ( t->inplace || t->own ) && !t->multi ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
     for(;;) {
@@ -460,11 +467,11 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
     if( err ) return err;
   }
   while( !t->open ) {
-    if( t->multi ) {
-      /* a free shared buffer (the engine is chosen when the batch closes) */
+    if( t->multi || t->own ) {
+      /* a free buffer (multi: the engine is chosen when the batch closes) */
       if( !t->pool.empty() ) {
         fd_vt_batch * b = t->pool.back(); t->pool.pop_back();
-        b->used = 0; b->nsig = 0; b->ticket = 0;
+        b->used = 0; b->nsig = 0; b->ticket = 0; b->alen = 0; b->blob2 = NULL;
         t->open = b;
         break;
       }
@@ -494,8 +501,8 @@ static int fd_vt_reserve( fd_verify_tile_t * t, unsigned long nsig, unsigned lon
   return 0;
 }
 
-FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
-                                                 fd_verify_tile_publish_fn publish, void * ctx ) {
+static fd_verify_tile_t * fd_vt_new_base( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
+                                          fd_verify_tile_publish_fn publish, void * ctx ) {
   if( !gpu ) return NULL;
   fd_verify_tile_cfg_t c = { 0UL, 16UL, 64UL, 0L };
   if( cfg ) c = *cfg;
@@ -514,6 +521,44 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
   for( int i=0; i<depth; i++ ) { fd_vt_batch * b = new fd_vt_batch(); b->ticket = 0; t->pool.push_back( b ); }
   t->out.resize( maxs );
   memset( t->diag, 0, sizeof(t->diag) );
+  return t;
+}
+
+/* Copy mode.  Batches are built in depth + 2 buffers of the tile's own,
+   registered with the engine: the frags are copied once (into the buffer)
+   and the batch is DMA'd from there, blob and descriptors, so it holds a
+   ring slot only from its close to its poll.  With the engine's staged
+   slots instead, a batch holds its slot while it fills and until its
+   in-order publish: two tiles sharing an engine each keep a slot filling,
+   and at 30 M verifies/s the shared ring of eight ran full 13-166 K times a
+   minute against 0.2-41 K in place (profiles/r06_task_c5_60s*.jsonl).  If
+   the registration fails (or $FD_VERIFY_TILE_COPY_STAGED is 1) the tile
+   uses the staged slots. */
+FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_verify_tile_cfg_t const * cfg,
+                                                 fd_verify_tile_publish_fn publish, void * ctx ) {
+  fd_verify_tile_t * t = fd_vt_new_base( gpu, cfg, publish, ctx );
+  if( !t ) return NULL;
+  char const * st = getenv( "FD_VERIFY_TILE_COPY_STAGED" );
+  if( st && st[0] == '1' ) return t;
+  unsigned long const blob_room = ( t->max_blob + 64UL + 63UL ) & ~63UL;
+  unsigned long const desc_room = ( t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL ) & ~63UL;
+  unsigned long const per = blob_room + desc_room;
+  int const nb = fd_ed25519_gpu_depth( gpu ) + 2;
+  void * r = NULL;
+  if( posix_memalign( &r, 4096UL, per * (unsigned long)nb ) ) return t;
+  memset( r, 0, per * (unsigned long)nb );
+  if( fd_ed25519_gpu_register( gpu, r, per * (unsigned long)nb ) ) { free( r ); return t; }
+  t->own = 1; t->region = (uint8_t *)r; t->region_sz = per * (unsigned long)nb;
+  for( fd_vt_batch * b : t->pool ) delete b;
+  t->pool.clear();
+  for( int k=0; k<nb; k++ ) {
+    fd_vt_batch * b = new fd_vt_batch();
+    b->blob = t->region + per * (unsigned long)k;
+    b->desc = (fd_ed25519_gpu_desc_t *)( b->blob + blob_room );
+    b->ticket = 0; b->used = 0; b->nsig = 0; b->alen = 0; b->blob2 = NULL;
+    t->pool.push_back( b );
+    t->all.push_back( b );
+  }
   return t;
 }
 
@@ -624,7 +669,7 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_inplace( fd_ed25519_gpu_t * gpu,
                                                          void const * region, unsigned long region_sz,
                                                          fd_verify_tile_publish_fn publish, void * ctx ) {
   if( !gpu || !region || !region_sz ) return NULL;
-  fd_verify_tile_t * t = fd_verify_tile_new( gpu, cfg, publish, ctx );
+  fd_verify_tile_t * t = fd_vt_new_base( gpu, cfg, publish, ctx );
   if( !t ) return NULL;
   if( fd_ed25519_gpu_register( gpu, (void *)region, region_sz ) ) { fd_verify_tile_delete( t ); return NULL; }
   t->inplace = 1; t->ip_region = (uint8_t const *)region; t->ip_region_sz = region_sz;
@@ -687,6 +732,27 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
       }
     }
     free( t->region );
+    for( fd_vt_batch * b : t->all ) delete b;
+    fd_vt_tcache_delete( t->tc );
+    delete t;
+    return;
+  }
+  if( t->own ) {
+    /* as in place: the buffers must not go while a slot still DMAs them;
+       left registered (and allocated) if the device never lets go */
+    while( !t->inflight.empty() ) {
+      fd_vt_batch * b = t->inflight.front(); t->inflight.pop_front();
+      fd_ed25519_gpu_poll( t->gpu, b->ticket, NULL, 1 );
+    }
+    int r = fd_ed25519_gpu_unregister( t->gpu, t->region );
+    long to = fd_ed25519_gpu_timeout( t->gpu );
+    unsigned long t0 = fd_vt_now();
+    while( r == FD_ED25519_ERR_GPU && to >= 0 && fd_vt_now() - t0 < (unsigned long)to ) {
+      struct timespec ts = { 0, 1000000L }; nanosleep( &ts, NULL );
+      r = fd_ed25519_gpu_unregister( t->gpu, t->region );
+    }
+    if( r ) fprintf( stderr, "fd_verify_tile_delete: batch buffers %p still in use by the device: leaked\n", (void *)t->region );
+    else free( t->region );
     for( fd_vt_batch * b : t->all ) delete b;
     fd_vt_tcache_delete( t->tc );
     delete t;

@@ -270,8 +270,9 @@ int fd_ed25519_gpu_cu_groups    ( fd_ed25519_gpu_t const * gpu );
    (hipHostRegister; call before sandboxing, e.g. on the tile's input
    dcache).  A submitted blob lying inside a registered region is copied
    to the device straight from the caller's bytes -- no staging memcpy --
-   so those bytes must stay unchanged until the batch is polled.  Up to
-   16 regions per engine. */
+   so those bytes must stay unchanged until the batch is polled; so are
+   its descriptors when they lie in a registered region too.  Up to 16
+   regions per engine. */
 int fd_ed25519_gpu_register  ( fd_ed25519_gpu_t * gpu, void * host, unsigned long sz );
 int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * gpu, void * host );
 

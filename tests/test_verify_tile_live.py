@@ -133,14 +133,20 @@ def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["copy", "inplace"])
+@pytest.mark.parametrize("mode", ["copy", "copy_staged", "inplace"])
 def test_two_tiles_one_engine(ref, tmp_path, mode):
     """Two verify tile tasks sharing one engine (fd_verify_tile_args_t.
     shared_gpu), each with its own producer and link, at 10 M verifies/s
     for 2 s: every publish carries exactly its seq's bytes and is one the
-    reference publishes, and nothing is lost (a copying tile publishes from
-    the ring slot it staged the frags in, kept lent past the poll,
-    FD_ED25519_GPU_POLL_KEEP)."""
+    reference publishes, and nothing is lost.  copy: the tiles build
+    batches in their own registered buffers; copy_staged
+    ($FD_VERIFY_TILE_COPY_STAGED=1): in the engine's staged slots, a
+    copying tile publishing from the slot it staged, kept lent past the
+    poll (FD_ED25519_GPU_POLL_KEEP)."""
+    env = None
+    if mode == "copy_staged":
+        env = dict(os.environ, FD_VERIFY_TILE_COPY_STAGED="1")
+        mode = "copy"
     frags, ok = _cyclic_corpus(ref, 20000, 73)
     p = str(tmp_path / "frags.bin")
     write_frags(p, frags)
@@ -148,7 +154,7 @@ def test_two_tiles_one_engine(ref, tmp_path, mode):
     ok.astype(np.uint8).tofile(ex)
     spf = np.mean([f[((int.from_bytes(f[-2:], "little") + 1) & ~1) + 1] for f in frags])
     d = run(_exe(), p, mode=mode, rate=10e6 / spf / 2, seconds=2, tiles=2, share=1, depth=16384, batch=4096,
-            eng_depth=8, expect=ex, timeout=240, **_pin(4))
+            eng_depth=8, expect=ex, timeout=240, env=env, **_pin(4))
     assert d["rc"] == 0 and d["booted"] == 1 and d["shared_engine"] == 1, d
     assert d["mismatch"] == 0 and d["false_pub"] == 0 and d["order_err"] == 0, d
     if d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0:

@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--share", type=int, default=0, help="1: the tiles share one engine (fd_verify_tile_args_t.shared_gpu)")
     ap.add_argument("--rt", type=int, default=0, help="1: the harness's spinning threads ask for SCHED_FIFO (reported as rt_threads)")
     ap.add_argument("--sample", type=int, default=0, help="1: sample where tile 0's thread waits (tile0_syscall_samples)")
+    ap.add_argument("--copy-staged", type=int, default=0,
+                    help="1: copying tiles build batches in the engine's staged slots ($FD_VERIFY_TILE_COPY_STAGED)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -89,12 +91,14 @@ def main():
             if pin:
                 kw["cpus"] = pin
             t0 = time.time()
-            d = run(exe, fp, timeout=a.seconds + 120, **kw)
+            env = dict(os.environ, FD_VERIFY_TILE_COPY_STAGED="1") if a.copy_staged else None
+            d = run(exe, fp, timeout=a.seconds + 120, env=env, **kw)
             if "error" in d:      # the harness refused the configuration (e.g. an engine depth past the maximum)
                 print(json.dumps({"error": d["error"], "config": kw, "rc": d["rc"]}), flush=True)
                 continue
             d.pop("stderr", None)
-            d.update({"offered_verifies_s": r, "sigs_per_frag": spf, "corpus_frags": len(frags),
+            d.update({"copy_buffers": "engine staged slots" if a.copy_staged else "tile's own registered buffers",
+                      "offered_verifies_s": r, "sigs_per_frag": spf, "corpus_frags": len(frags),
                       "corpus_reference_pass": int(ok.sum()), "cpus": pin, "wall_s": time.time() - t0,
                       "kernels_id": fa.kernels_id(),
                       "reference_check": {"publishes_checked": d["pub"], "false_pub": d["false_pub"],
