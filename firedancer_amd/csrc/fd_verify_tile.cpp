@@ -673,17 +673,24 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new_inplace( fd_ed25519_gpu_t * gpu,
   if( !t ) return NULL;
   if( fd_ed25519_gpu_register( gpu, (void *)region, region_sz ) ) { fd_verify_tile_delete( t ); return NULL; }
   t->inplace = 1; t->ip_region = (uint8_t const *)region; t->ip_region_sz = region_sz;
-  /* batches own their descriptor arrays (the engine copies them into its
-     slot at submit); 2 x depth so the next batch fills while the ring is
-     full */
+  /* batches own their descriptor arrays, 2 x depth so the next batch
+     fills while the ring is full: one allocation registered with the
+     engine, so a submit DMAs them from where they lie instead of copying
+     them into its slot under the ring lock (unregistered, e.g. where the
+     registration fails, the engine copies them) */
   for( fd_vt_batch * b : t->pool ) delete b;
   t->pool.clear();
   int nb = 2 * fd_ed25519_gpu_depth( gpu );
+  unsigned long const dsz = ( t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL ) & ~63UL;
+  void * r = NULL;
+  if( posix_memalign( &r, 4096UL, dsz * (unsigned long)nb ) ) { fd_verify_tile_delete( t ); return NULL; }
+  memset( r, 0, dsz * (unsigned long)nb );
+  t->region = (uint8_t *)r; t->region_sz = dsz * (unsigned long)nb;
+  t->reg_ok[0] = !fd_ed25519_gpu_register( gpu, r, t->region_sz );
   for( int i=0; i<nb; i++ ) {
     fd_vt_batch * b = new fd_vt_batch();
-    b->desc = (fd_ed25519_gpu_desc_t *)malloc( t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) );
+    b->desc = (fd_ed25519_gpu_desc_t *)( t->region + dsz * (unsigned long)i );
     b->blob = NULL; b->ticket = 0; b->used = 0; b->nsig = 0;
-    if( !b->desc ) { delete b; fd_verify_tile_delete( t ); return NULL; }
     t->pool.push_back( b );
     t->all.push_back( b );
   }
@@ -716,7 +723,11 @@ FD_EXPORT void fd_verify_tile_delete( fd_verify_tile_t * t ) {
     }
     if( r ) fprintf( stderr, "fd_verify_tile_delete: input region %p still in use by the device: left registered (leaked)\n",
                      (void const *)t->ip_region );
-    for( fd_vt_batch * b : t->all ) { free( b->desc ); delete b; }
+    if( t->region ) {   /* the descriptor arrays (idle now, or leaked with the input region) */
+      int rd = t->reg_ok[0] ? fd_ed25519_gpu_unregister( t->gpu, t->region ) : 0;
+      if( !r && !rd ) free( t->region );
+    }
+    for( fd_vt_batch * b : t->all ) delete b;
     fd_vt_tcache_delete( t->tc );
     delete t;
     return;
