@@ -140,6 +140,7 @@ extern "C" int fd_ed25519_gpu_wait_selftest( long timeout_ns, long ready_after_n
 #define FD_CODE_PENDING ((int32_t)0x7eadc0de)
 
 static inline unsigned long fd_desc_off( unsigned long blob_sz ) { return (blob_sz + FD_BLOB_PAD + 15UL) & ~15UL; }
+extern "C" unsigned long fd_ed25519_gpu_desc_offset( unsigned long blob_sz ) { return fd_desc_off( blob_sz ); }
 
 struct fd_ed25519_gpu_slot {
   /* pinned host staging */
@@ -876,6 +877,9 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   /* descriptors in a registered region too go from where they lie (a
      verify tile building batches in its own registered buffers) */
   int const ddirect = direct && fd_registered( g, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
+  /* ... and packed right after the blob in the device's layout: one copy */
+  int const packed = ddirect && !blob2_sz && (uint8_t const *)desc == (uint8_t const *)blob + doff
+                  && fd_registered( g, blob, doff + n * sizeof(fd_ed25519_gpu_desc_t) );
   if( direct && !ddirect ) memcpy( sl->h_desc, desc, n * sizeof(fd_ed25519_gpu_desc_t) );
   else {
     if( sl->h_blob != blob ) memcpy( sl->h_blob, blob, sz0 );
@@ -891,7 +895,10 @@ static int fd_slot_enqueue_( fd_ed25519_gpu_t * g, fd_ed25519_gpu_slot * sl, uns
   int others = sl->mstream && n <= g->mask_max && (g->group_always || busy);
   hipStream_t st = others ? sl->mstream : sl->stream;
   *used = st;
-  if( direct ) {
+  if( packed ) {
+    if( (e = hipMemcpyAsync( sl->d_blob, blob, doff + n * sizeof(fd_ed25519_gpu_desc_t), hipMemcpyHostToDevice, st )) != hipSuccess )
+      return fd_gpu_fail( "H2D blob+desc (registered)", e );
+  } else if( direct ) {
     if( (e = hipMemcpyAsync( sl->d_blob, blob, sz0, hipMemcpyHostToDevice, st )) != hipSuccess )
       return fd_gpu_fail( "H2D blob (registered)", e );
     if( blob2_sz && (e = hipMemcpyAsync( sl->d_blob + sz0, blob2, blob2_sz, hipMemcpyHostToDevice, st )) != hipSuccess )

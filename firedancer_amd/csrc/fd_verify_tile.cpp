@@ -364,9 +364,18 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
     for(;;) {
+      fd_ed25519_gpu_desc_t const * desc = b->desc;
+      if( t->own ) {
+        /* the descriptors packed after the blob in the device's layout (the
+           padding zeroed): the engine sends blob and descriptors in one copy */
+        unsigned long doff = fd_ed25519_gpu_desc_offset( b->used );
+        memset( b->blob + b->used, 0, doff - b->used );
+        memcpy( b->blob + doff, b->desc, b->nsig * sizeof(fd_ed25519_gpu_desc_t) );
+        desc = (fd_ed25519_gpu_desc_t const *)( b->blob + doff );
+      }
       auto try_ = [&]() {
-        return b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, b->desc, &b->ticket )
-                       : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, b->desc, &b->ticket );
+        return b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, desc, &b->ticket )
+                       : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, desc, &b->ticket );
       };
       int r = try_();
       if( r == 1 ) break;
@@ -540,7 +549,10 @@ FD_EXPORT fd_verify_tile_t * fd_verify_tile_new( fd_ed25519_gpu_t * gpu, fd_veri
   if( !t ) return NULL;
   char const * st = getenv( "FD_VERIFY_TILE_COPY_STAGED" );
   if( st && st[0] == '1' ) return t;
-  unsigned long const blob_room = ( t->max_blob + 64UL + 63UL ) & ~63UL;
+  /* per buffer: blob, its padding and packed descriptors (fd_vt_submit),
+     then the descriptors as rx writes them */
+  unsigned long const blob_room = ( fd_ed25519_gpu_desc_offset( t->max_blob )
+                                    + t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL ) & ~63UL;
   unsigned long const desc_room = ( t->batch_sigs * sizeof(fd_ed25519_gpu_desc_t) + 63UL ) & ~63UL;
   unsigned long const per = blob_room + desc_room;
   int const nb = fd_ed25519_gpu_depth( gpu ) + 2;

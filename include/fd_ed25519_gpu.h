@@ -129,6 +129,11 @@ fd_ed25519_gpu_delete( fd_ed25519_gpu_t * gpu );
 
 unsigned long fd_ed25519_gpu_max_sigs( fd_ed25519_gpu_t const * gpu );
 unsigned long fd_ed25519_gpu_max_blob( fd_ed25519_gpu_t const * gpu );
+/* Where a batch's descriptors go after its blob_sz bytes of blob (the
+   engine's device layout: blob, zero padding, descriptors).  A submitted
+   batch in a registered region whose descriptors lie packed there, with
+   the padding zeroed, goes to the device in one copy. */
+unsigned long fd_ed25519_gpu_desc_offset( unsigned long blob_sz );
 
 /* Descriptor bounds (every entry point): a descriptor whose signature,
    key or message does not lie inside blob[0, blob_sz) gets

@@ -81,6 +81,8 @@ extern "C" int hipDeviceGetPCIBusId( char * bus, int len, int device ) { (void)b
 extern "C" int hipSetDevice( int device ) { (void)device; return 0; }
 /* host regions (the verify tile's feeder mode registers its batch
    buffers): nothing to map on the CPU */
+/* the real engine's device layout (blob, 64 B of zero padding, descriptors) */
+extern "C" unsigned long fd_ed25519_gpu_desc_offset( unsigned long blob_sz ) { return ( blob_sz + 64UL + 15UL ) & ~15UL; }
 extern "C" int fd_ed25519_gpu_register( fd_ed25519_gpu_t * g, void * host, unsigned long sz ) { return ( !g || !host || !sz ) ? FD_ED25519_ERR_ARG : 0; }
 extern "C" int fd_ed25519_gpu_unregister( fd_ed25519_gpu_t * g, void * host ) { return ( !g || !host ) ? FD_ED25519_ERR_ARG : 0; }
 /* the node the multi-engine tests pretend to have */
