@@ -97,7 +97,9 @@ def main():
                 print(json.dumps({"error": d["error"], "config": kw, "rc": d["rc"]}), flush=True)
                 continue
             d.pop("stderr", None)
-            d.update({"copy_buffers": "engine staged slots" if a.copy_staged else "tile's own registered buffers",
+            if mode == "copy":
+                d["copy_buffers"] = "engine staged slots" if a.copy_staged else "tile's own registered buffers"
+            d.update({
                       "offered_verifies_s": r, "sigs_per_frag": spf, "corpus_frags": len(frags),
                       "corpus_reference_pass": int(ok.sum()), "cpus": pin, "wall_s": time.time() - t0,
                       "kernels_id": fa.kernels_id(),
