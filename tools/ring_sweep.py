@@ -32,7 +32,7 @@ def main():
         for g in [int(x) for x in a.groups.split(",")]:
             if g > d:
                 continue
-            wins = [int(x) for x in a.window_abs.split(",")] if a.window_abs else [int(x) * d for x in a.windows.split(",")]
+            wins = [int(x) for x in a.window_abs.replace("+", ",").split(",")] if a.window_abs else [int(x) * d for x in a.windows.split(",")]
             for w in wins:
                 if w > d:
                     continue
