@@ -560,6 +560,8 @@ def latency_legs(fa, corpus, a, device):
     t0 = time.time()
     exp = ring_reference_codes(ring, usable_cores())
     ref_s = time.time() - t0
+    global RING_CORES
+    RING_CORES = tuple(fa.quiet_cpus(2, device)) or None
     nb, nb2 = a.latency_batches, max(a.latency_batches // 2, 20)
     lat = ring_stream(fa, ring, device, nb, a.ring_depth, window=a.ring_window, expected=exp)
     lat["corpus"] = {"windows": RING_WINDOWS, "sigs": len(ring), "q2_at": list(RING_Q2_AT), "gen_s": gen_s,
@@ -601,6 +603,12 @@ def latency_legs(fa, corpus, a, device):
     return lat
 
 
+# the ring legs' two spinning host threads (the synthetic producer, the
+# per-GPU feeder) each on a quiet core of the GPU's NUMA node, as a
+# validator pins its tiles (fa.quiet_cpus); chosen once per run
+RING_CORES = None
+
+
 def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=True, seed=7, period_ns=0,
                 expected=None, batch_sigs=BATCH_SIGS, q2_at=RING_Q2_AT):
     """C2 at its own granularity: nb 4096-signature batches streamed through
@@ -628,12 +636,20 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                      (d["msg_off"].astype(np.int64) + d["msg_sz"]).max()))
         span = max(span, hi - lo + 64)
     eng = fa.Engine(device, max_sigs=BS, max_blob=span, depth=depth)
+    prev_aff = os.sched_getaffinity(0)
+    cores = RING_CORES
     try:
         if groups:
             eng.cu_groups = groups
         if register:
             eng.register(base.blob)
+        # the feeder thread takes the creating thread's CPUs (within the
+        # GPU's NUMA node); then this thread, the producer, moves to its own
+        if cores:
+            os.sched_setaffinity(0, {cores[1]})
         feeder = fa.Feeder(eng)
+        if cores:
+            os.sched_setaffinity(0, {cores[0]})
         starts = np.random.default_rng(seed).permutation(nwin).astype(np.uint64) * BS
         W = window or depth
         # untimed warm-up: two closed-loop passes over every window, so the
@@ -693,7 +709,8 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                "codes": hist, "reference_checked": expected is not None, "mismatches": mism,
                "label_check_mismatches": label_mism,
                # True only when every code was compared with the reference build's
-               "codes_ok": (complete and mism == 0) if expected is not None else (False if not complete else None)}
+               "codes_ok": (complete and mism == 0) if expected is not None else (False if not complete else None),
+               "host_cores": None if not cores else {"producer": cores[0], "feeder": cores[1]}}
         if period_ns:
             sl = (st["t_done_ns"] - st["t_sched_ns"]) * 1e-6
             offered = BS / (period_ns * 1e-9)
@@ -705,6 +722,7 @@ def ring_stream(fa, base, device, nb, depth, groups=None, window=None, register=
                        latency="scheduled arrival -> codes on the host (p50_ms/p99_ms: push -> codes)")
         return res
     finally:
+        os.sched_setaffinity(0, prev_aff)
         eng.close()
 
 

@@ -691,6 +691,58 @@ def numa_cpus(device: int) -> list:
     return sorted(cpus & os.sched_getaffinity(0))
 
 
+def _cpu_times() -> dict:
+    out = {}
+    for line in open("/proc/stat"):
+        if line.startswith("cpu") and line[3].isdigit():
+            f = line.split()
+            v = [int(x) for x in f[1:]]
+            out[int(f[0][3:])] = (v[3] + (v[4] if len(v) > 4 else 0), sum(v))   # (idle + iowait, total)
+    return out
+
+
+def _core_siblings(c: int) -> set:
+    try:
+        txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+    except OSError:
+        return {c}
+    sib = set()
+    for part in txt.split(","):
+        lo, _, hi = part.partition("-")
+        sib.update(range(int(lo), int(hi or lo) + 1))
+    return sib
+
+
+def quiet_cpus(n: int, device: int = 0, sample_s: float = 0.3) -> list:
+    """n CPUs for spinning host threads (tiles, feeders, producers): on the
+    device's NUMA node, not CPU 0, one per physical core, the least busy over
+    a short /proc/stat sample counting each core's other hardware threads --
+    on a shared host other work lands on some CPUs, and a spinning thread
+    that shares its core with it stalls for milliseconds.  [] if fewer."""
+    import time
+    cand = [c for c in (numa_cpus(device) or sorted(os.sched_getaffinity(0))) if c != 0]
+    if len(cand) < n:
+        return []
+    t0 = _cpu_times()
+    time.sleep(sample_s)
+    t1 = _cpu_times()
+
+    def busy(c):
+        if c not in t0 or c not in t1 or t1[c][1] <= t0[c][1]:
+            return 0.0
+        return 1.0 - (t1[c][0] - t0[c][0]) / (t1[c][1] - t0[c][1])
+    score = {c: sum(busy(x) for x in _core_siblings(c)) for c in cand}
+    pick, used = [], set()
+    for c in sorted(cand, key=lambda c: (score[c], c)):
+        if c in used:
+            continue
+        pick.append(c)
+        used |= _core_siblings(c)
+        if len(pick) == n:
+            return pick
+    return []
+
+
 def sign_batch(seeds: np.ndarray, blob: np.ndarray, msg_off: np.ndarray, msg_sz: np.ndarray, nthreads: int = 8):
     """Host signer (test-data generation only): returns (pub[n,32], sig[n,64])."""
     seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)

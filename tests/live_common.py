@@ -15,58 +15,12 @@ DIAG = ("IN_BACKP", "BACKP_CNT", "HA_FILT_CNT", "HA_FILT_SZ", "SV_FILT_CNT", "SV
         "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT", "RING_FULL_CNT", "OVRN_CNT", "AGE_CNT")
 
 
-def _cpu_times():
-    out = {}
-    for line in open("/proc/stat"):
-        if line.startswith("cpu") and line[3].isdigit():
-            f = line.split()
-            v = [int(x) for x in f[1:]]
-            out[int(f[0][3:])] = (v[3] + (v[4] if len(v) > 4 else 0), sum(v))   # (idle + iowait, total)
-    return out
-
-
-def _siblings(c):
-    try:
-        txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
-    except OSError:
-        return {c}
-    sib = set()
-    for part in txt.split(","):
-        lo, _, hi = part.partition("-")
-        sib.update(range(int(lo), int(hi or lo) + 1))
-    return sib
-
-
 def quiet_cpus(n, device=0, sample_s=0.3):
-    """n CPUs for the harness's spinning threads (producer k, tile k ...):
-    on the GPU's NUMA node, not CPU 0, one per physical core, the least
-    busy over a short sample of /proc/stat counting the core's other
-    hardware threads -- a shared host's other work lands on some CPUs, and
-    a spinning tile that shares its core with it stalls for milliseconds.
-    -> "c0,c1,..." or None"""
-    import time
+    """n quiet CPUs of the GPU's NUMA node as "c0,c1,..." (firedancer_amd.
+    quiet_cpus), or None"""
     import firedancer_amd as fa
-    cand = [c for c in (fa.numa_cpus(device) or sorted(os.sched_getaffinity(0))) if c != 0]
-    if len(cand) < n:
-        return None
-    t0 = _cpu_times()
-    time.sleep(sample_s)
-    t1 = _cpu_times()
-
-    def busy(c):
-        if c not in t0 or c not in t1 or t1[c][1] <= t0[c][1]:
-            return 0.0
-        return 1.0 - (t1[c][0] - t0[c][0]) / (t1[c][1] - t0[c][1])
-    score = {c: sum(busy(s) for s in _siblings(c)) for c in cand}
-    pick, used = [], set()
-    for c in sorted(cand, key=lambda c: (score[c], c)):
-        if c in used:
-            continue
-        pick.append(c)
-        used |= _siblings(c)
-        if len(pick) == n:
-            return ",".join(str(x) for x in pick)
-    return None
+    pick = fa.quiet_cpus(n, device, sample_s)
+    return ",".join(str(x) for x in pick) if pick else None
 
 
 def write_frags(path, frags):
