@@ -363,16 +363,16 @@ static int fd_vt_submit( fd_verify_tile_t * t ) {
   if( ( t->inplace || t->own ) && !t->multi ) {
     /* the span goes to the device from where it lies (a registered region:
        no staging copy); a full ring publishes the oldest batch first */
+    fd_ed25519_gpu_desc_t const * desc = b->desc;
+    if( t->own ) {
+      /* the descriptors packed after the blob in the device's layout (the
+         padding zeroed): the engine sends blob and descriptors in one copy */
+      unsigned long doff = fd_ed25519_gpu_desc_offset( b->used );
+      memset( b->blob + b->used, 0, doff - b->used );
+      memcpy( b->blob + doff, b->desc, b->nsig * sizeof(fd_ed25519_gpu_desc_t) );
+      desc = (fd_ed25519_gpu_desc_t const *)( b->blob + doff );
+    }
     for(;;) {
-      fd_ed25519_gpu_desc_t const * desc = b->desc;
-      if( t->own ) {
-        /* the descriptors packed after the blob in the device's layout (the
-           padding zeroed): the engine sends blob and descriptors in one copy */
-        unsigned long doff = fd_ed25519_gpu_desc_offset( b->used );
-        memset( b->blob + b->used, 0, doff - b->used );
-        memcpy( b->blob + doff, b->desc, b->nsig * sizeof(fd_ed25519_gpu_desc_t) );
-        desc = (fd_ed25519_gpu_desc_t const *)( b->blob + doff );
-      }
       auto try_ = [&]() {
         return b->alen ? fd_ed25519_gpu_try_submit2( t->gpu, b->nsig, b->blob, b->alen, b->blob2, b->used - b->alen, desc, &b->ticket )
                        : fd_ed25519_gpu_try_submit( t->gpu, b->nsig, b->blob, b->used, desc, &b->ticket );
