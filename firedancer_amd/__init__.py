@@ -713,12 +713,23 @@ def _core_siblings(c: int) -> set:
     return sib
 
 
-def quiet_cpus(n: int, device: int = 0, sample_s: float = 0.3) -> list:
+def _l3_group(c: int) -> str:
+    try:
+        return open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read().strip()
+    except OSError:
+        return ""
+
+
+def quiet_cpus(n: int, device: int = 0, sample_s: float = 0.3, pairs: bool = True) -> list:
     """n CPUs for spinning host threads (tiles, feeders, producers): on the
     device's NUMA node, not CPU 0, one per physical core, the least busy over
     a short /proc/stat sample counting each core's other hardware threads --
     on a shared host other work lands on some CPUs, and a spinning thread
-    that shares its core with it stalls for milliseconds.  [] if fewer."""
+    that shares its core with it stalls for milliseconds.  pairs: CPUs
+    2k and 2k+1 (a producer and its consumer) share a last-level cache, so
+    the bytes one writes reach the other without crossing chiplets (on the
+    GPU box's EPYC one CCD of 8 cores per L3).  [] if that many cannot be
+    found."""
     import time
     cand = [c for c in (numa_cpus(device) or sorted(os.sched_getaffinity(0))) if c != 0]
     if len(cand) < n:
@@ -732,8 +743,39 @@ def quiet_cpus(n: int, device: int = 0, sample_s: float = 0.3) -> list:
             return 0.0
         return 1.0 - (t1[c][0] - t0[c][0]) / (t1[c][1] - t0[c][1])
     score = {c: sum(busy(x) for x in _core_siblings(c)) for c in cand}
+    order = sorted(cand, key=lambda c: (score[c], c))
     pick, used = [], set()
-    for c in sorted(cand, key=lambda c: (score[c], c)):
+    if pairs and n >= 2:
+        # quietest pairs first, each pair from one L3 group
+        while len(pick) + 2 <= n:
+            best = None
+            groups = {}
+            for c in order:
+                if c in used:
+                    continue
+                groups.setdefault(_l3_group(c), []).append(c)
+            for g, cs in groups.items():
+                two = []
+                seen = set()
+                for c in cs:                          # one per physical core
+                    if c in seen:
+                        continue
+                    two.append(c)
+                    seen |= _core_siblings(c)
+                    if len(two) == 2:
+                        break
+                if len(two) == 2 and (best is None or score[two[0]] + score[two[1]] < best[0]):
+                    best = (score[two[0]] + score[two[1]], two)
+            if best is None:
+                break
+            for c in best[1]:
+                pick.append(c)
+                used |= _core_siblings(c)
+        if len(pick) == n:
+            return pick
+        if len(pick) + 1 != n:
+            pick, used = [], set()
+    for c in order:
         if c in used:
             continue
         pick.append(c)

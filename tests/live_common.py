@@ -15,11 +15,11 @@ DIAG = ("IN_BACKP", "BACKP_CNT", "HA_FILT_CNT", "HA_FILT_SZ", "SV_FILT_CNT", "SV
         "PUB_CNT", "PUB_SZ", "BAD_CNT", "SIG_CNT", "BATCH_CNT", "RING_FULL_CNT", "OVRN_CNT", "AGE_CNT")
 
 
-def quiet_cpus(n, device=0, sample_s=0.3):
+def quiet_cpus(n, device=0, sample_s=0.3, pairs=True):
     """n quiet CPUs of the GPU's NUMA node as "c0,c1,..." (firedancer_amd.
-    quiet_cpus), or None"""
+    quiet_cpus: producer k and tile k share a last-level cache), or None"""
     import firedancer_amd as fa
-    pick = fa.quiet_cpus(n, device, sample_s)
+    pick = fa.quiet_cpus(n, device, sample_s, pairs)
     return ",".join(str(x) for x in pick) if pick else None
 
 

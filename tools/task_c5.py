@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--sample", type=int, default=0, help="1: sample where tile 0's thread waits (tile0_syscall_samples)")
     ap.add_argument("--copy-staged", type=int, default=0,
                     help="1: copying tiles build batches in the engine's staged slots ($FD_VERIFY_TILE_COPY_STAGED)")
+    ap.add_argument("--l3-pairs", type=int, default=1,
+                    help="1: producer k and tile k on cores sharing a last-level cache (fa.quiet_cpus pairs)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import ctypes
@@ -80,7 +82,7 @@ def main():
     write_frags(fp, frags)
     ok.astype(np.uint8).tofile(ex)
     from live_common import quiet_cpus
-    pin = quiet_cpus(2 * a.tiles)   # producer k, tile k: the quietest cores of the GPU's NUMA node
+    pin = quiet_cpus(2 * a.tiles, pairs=bool(a.l3_pairs))   # producer k, tile k: the quietest cores of the GPU's NUMA node
     exe = os.path.join(ROOT, "firedancer_amd", "vt_live")
     out = open(a.out, "a") if a.out else None
     # ',' or '+' between values ('+' survives tools/gpu.sh's py= step)
@@ -99,6 +101,7 @@ def main():
             d.pop("stderr", None)
             if mode == "copy":
                 d["copy_buffers"] = "engine staged slots" if a.copy_staged else "tile's own registered buffers"
+            d["l3_pairs"] = bool(a.l3_pairs)
             d.update({
                       "offered_verifies_s": r, "sigs_per_frag": spf, "corpus_frags": len(frags),
                       "corpus_reference_pass": int(ok.sum()), "cpus": pin, "wall_s": time.time() - t0,
