@@ -26,6 +26,7 @@
 #include <atomic>
 #include <map>
 #include "fd_ed25519_gpu_private.h"
+#include "fd_ed25519_gpu_diag.h"
 
 #define FD_GPU_DEPTH_DEFAULT 3
 #define FD_GPU_DEPTH_MAX     8
@@ -702,6 +703,19 @@ static fd_ed25519_gpu_slot * fd_free_slot( fd_ed25519_gpu_t * g, void const * bl
   return sl;
 }
 extern "C" int fd_ed25519_gpu_device( fd_ed25519_gpu_t const * g ) { return g ? g->device : -1; }
+
+extern "C" int fd_ed25519_gpu_slot_states( fd_ed25519_gpu_t * g, int * out, int max ) {
+  if( !g || !out || max <= 0 ) return 0;
+  std::lock_guard<fd_ring_lock> guard( g->lock );
+  int k = 0;
+  for( ; k<g->depth && k<max; k++ ) {
+    fd_ed25519_gpu_slot const * sl = &g->slot[k];
+    out[k] = ( sl->ticket ? 1 : 0 ) | ( sl->staged ? 2 : 0 ) | ( sl->retiring ? 4 : 0 ) | ( sl->orphan ? 8 : 0 )
+           | ( sl->early ? 16 : 0 ) | ( hipEventQuery( sl->done ) == hipSuccess ? 32 : 0 );
+  }
+  (void)hipGetLastError();
+  return k;
+}
 
 /* The device-resident path.  Descriptors are bounds-checked on the device
    against blob_sz (fd_k_prep reports FD_ED25519_ERR_ARG, nothing reads

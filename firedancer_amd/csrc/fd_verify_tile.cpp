@@ -996,3 +996,13 @@ FD_EXPORT void fd_verify_tile_diag( fd_verify_tile_t const * t, unsigned long * 
   diag[ FD_VERIFY_TILE_DIAG_IN_BACKP  ] = 0UL;   /* flow control lives in the task's run loop */
   diag[ FD_VERIFY_TILE_DIAG_BACKP_CNT ] = 0UL;
 }
+
+FD_EXPORT void fd_verify_tile_state( fd_verify_tile_t const * t, unsigned long * out ) {
+  fd_vt_batch const * b = t->open;
+  out[0] = b ? b->nsig : 0UL;
+  out[1] = ( b && b->nsig ) ? fd_vt_now() - b->t_open : 0UL;
+  out[2] = t->inflight.size();
+  out[3] = t->pool.size();
+  out[4] = t->rx_cnt;
+  out[5] = t->inflight.empty() ? 0UL : t->inflight.front()->ticket;
+}

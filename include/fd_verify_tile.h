@@ -262,6 +262,13 @@ unsigned long fd_verify_tile_held( fd_verify_tile_t const * tile );
 /* Snapshot of the diagnostic counters (FD_VERIFY_TILE_DIAG_CNT slots). */
 void fd_verify_tile_diag( fd_verify_tile_t const * tile, unsigned long * diag );
 
+/* The tile's batch state, for a harness whose tile thread outlived its
+   time limit (not synchronised with the tile's thread: call it only once
+   that thread is known to be stuck or stopped): out[6] = { signatures in
+   the open batch, its age in ns, batches in flight, free batch buffers,
+   frags received, ticket of the oldest batch in flight }. */
+void fd_verify_tile_state( fd_verify_tile_t const * tile, unsigned long * out );
+
 /* ---- The tile as a task (fd_frank_task_t shape, fd_frank.h:29-45) -----
 
    fd_verify_tile_task.init creates all device state (engine: HIP

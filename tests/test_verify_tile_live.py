@@ -54,7 +54,7 @@ def test_task_live_producer_bounded_latency(ref, tmp_path, mode, rate, n_sigs):
     pin = _pin()
     t0 = os.times()
     d = run(_exe(), p, mode=mode, rate=rate, count=len(frags), depth=16384, batch=4096, eng_depth=8, pubout=po,
-            timeout=240, **pin)
+            timeout=150, **pin)
     t1 = os.times()
     # this (parent) process's own CPU use while the harness ran: threads of
     # earlier tests still spinning here would compete with the harness
@@ -113,7 +113,7 @@ def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
     ex = str(tmp_path / "expect.bin")
     ok.astype(np.uint8).tofile(ex)
     n = 200_000
-    free = run(_exe(), p, mode="inplace", rate=0, count=n, depth=16384, batch=65536, eng_depth=3, expect=ex, timeout=240)
+    free = run(_exe(), p, mode="inplace", rate=0, count=n, depth=16384, batch=65536, eng_depth=3, expect=ex, timeout=150)
     assert free["rc"] == 0 and free["booted"] == 1, free
     assert free["mismatch"] == 0 and free["false_pub"] == 0 and free["order_err"] == 0, free
     assert free["pub"] <= free["taken_pass_expected"]
@@ -125,7 +125,7 @@ def test_task_inplace_overrun_never_publishes_overwritten_bytes(ref, tmp_path):
     print("free-running producer:", {k: free[k] for k in ("produced", "taken", "pub", "ovrnp", "ovrnr")},
           "OVRN_CNT", free["diag"]["OVRN_CNT"], "batches", free["diag"]["BATCH_CNT"])
     cred = run(_exe(), p, mode="inplace", rate=0, count=n, depth=16384, batch=65536, eng_depth=3, expect=ex, credit=1,
-               timeout=240)
+               timeout=150)
     assert cred["rc"] == 0 and cred["booted"] == 1, cred
     assert cred["taken"] == n and cred["ovrnp"] == 0 and cred["ovrnr"] == 0 and cred["diag"]["OVRN_CNT"] == 0, cred
     assert cred["mismatch"] == 0 and cred["false_pub"] == 0 and cred["pub"] == cred["taken_pass_expected"], cred
@@ -154,7 +154,7 @@ def test_two_tiles_one_engine(ref, tmp_path, mode):
     ok.astype(np.uint8).tofile(ex)
     spf = np.mean([f[((int.from_bytes(f[-2:], "little") + 1) & ~1) + 1] for f in frags])
     d = run(_exe(), p, mode=mode, rate=10e6 / spf / 2, seconds=2, tiles=2, share=1, depth=16384, batch=4096,
-            eng_depth=8, expect=ex, timeout=240, env=env, **_pin(4))
+            eng_depth=8, expect=ex, timeout=150, env=env, **_pin(4))
     assert d["rc"] == 0 and d["booted"] == 1 and d["shared_engine"] == 1, d
     assert d["mismatch"] == 0 and d["false_pub"] == 0 and d["order_err"] == 0, d
     if d["diag"]["OVRN_CNT"] == 0 and d["ovrnp"] == 0 and d["ovrnr"] == 0:

@@ -52,6 +52,7 @@
 #include <vector>
 #include <string>
 #include "fd_verify_tile.h"
+#include "fd_ed25519_gpu_diag.h"
 
 #ifdef VT_LIVE_FAKE
 extern "C" void fake_engine_cheap_default( int on );
@@ -281,6 +282,20 @@ static int wait_signal( fd_verify_tile_cnc_t * c, unsigned long want, double sec
   return 1;
 }
 
+/* the shared engine's ring slots (fd_ed25519_gpu_slot_states bits), to
+   stderr: where the tiles' batches stand when a run stalls */
+static void slot_states( fd_ed25519_gpu_t * g ) {
+#ifndef VT_LIVE_FAKE
+  if( !g ) return;
+  int st[64];
+  int n = fd_ed25519_gpu_slot_states( g, st, 64 );
+  fprintf( stderr, " | slots" );
+  for( int s=0; s<n; s++ ) fprintf( stderr, " %02x", st[s] );
+#else
+  (void)g;
+#endif
+}
+
 static double pct_ms( fd_verify_tile_lat_t const * h, double q ) {
   if( !h->cnt ) return -1.;
   unsigned long want = (unsigned long)( q * (double)h->cnt ), acc = 0;
@@ -446,6 +461,7 @@ int main( int argc, char ** argv ) {
       for( int k=0; k<tiles; k++ )
         fprintf( stderr, " | tile %d produced=%lu want=%lu taken=%lu pub=%lu signal=%lu", k, T[k]->L.produced.load(),
                  T[k]->L.want_a.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load(), sig_load( &T[k]->cnc ) );
+      slot_states( shared );
       fprintf( stderr, "\n" );
     }
   } );
@@ -495,6 +511,7 @@ int main( int argc, char ** argv ) {
      tile that holds a partial batch until HALT never gets there) */
   unsigned long t_wait = now_ns();
   double settle_s = atof( arg( argc, argv, "settle_s", "10" ) );
+  double const halt_s = atof( arg( argc, argv, "halt_s", "40" ) );   /* HALT -> BOOT, all tiles */
   for( int k=0; k<tiles; k++ ) {
     live & L = T[k]->L;
     unsigned long produced = L.produced.load();
@@ -529,7 +546,36 @@ int main( int argc, char ** argv ) {
     if( running[k] ) sig_store( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_HALT );
     else booted = 0;
   }
-  for( int k=0; k<tiles; k++ ) if( running[k] ) booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, 60. );
+  /* every halted task back to BOOT within one deadline; else report where
+     each tile stands (its batch state, the engine's slots) and leave
+     without joining the stuck threads (a hang fails fast, with its state) */
+  {
+    unsigned long const th = now_ns();
+    for( int k=0; k<tiles; k++ ) {
+      if( !running[k] ) continue;
+      double left = halt_s - (double)( now_ns() - th ) * 1e-9;
+      booted &= wait_signal( &T[k]->cnc, FD_VERIFY_TILE_SIGNAL_BOOT, left > 0. ? left : 0. );
+    }
+    int stuck = 0;
+    for( int k=0; k<tiles; k++ ) stuck |= running[k] && sig_load( &T[k]->cnc ) != FD_VERIFY_TILE_SIGNAL_BOOT;
+    if( stuck ) {
+      printf( "{\"error\": \"halt\", \"halt_s\": %.1f, \"tiles\": [", halt_s );
+      for( int k=0; k<tiles; k++ ) {
+        unsigned long st[6] = { 0 };
+        if( T[k]->a.tile ) fd_verify_tile_state( T[k]->a.tile, st );
+        printf( "%s{\"signal\": %lu, \"open_sigs\": %lu, \"open_age_ns\": %lu, \"inflight\": %lu, \"free\": %lu, "
+                "\"rx\": %lu, \"front_ticket\": %lu, \"produced\": %lu, \"taken\": %lu, \"pub\": %lu}",
+                k ? ", " : "", sig_load( &T[k]->cnc ), st[0], st[1], st[2], st[3], st[4], st[5],
+                T[k]->L.produced.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load() );
+      }
+      printf( "]}\n" );
+      fflush( stdout );
+      slot_states( shared );
+      fprintf( stderr, "\n" );
+      fflush( stderr );
+      _exit( 5 );
+    }
+  }
   unsigned long long clk[9] = { 0 };
 #ifndef VT_LIVE_FAKE
   if( shared || tiles == 1 ) fd_ed25519_gpu_dsm_clock( shared ? shared : T[0]->a.gpu, 0, clk );
