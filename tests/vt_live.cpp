@@ -452,11 +452,36 @@ int main( int argc, char ** argv ) {
   /* a monitor: every 5 s, to stderr, where main is and each tile's link
      and cnc state (a run that outlives its time limit then says where) */
   static std::atomic<int> phase( 1 ), mon_stop( 0 );
+  /* a run that is stuck (a HALT that does not come back, or the whole run
+     past its deadline): one JSON line with where each tile stands (its
+     batch state, read unsynchronised: its thread is stuck), the engine's
+     slot states to stderr, and out without joining the stuck threads */
+  auto stuck_exit = [&]( char const * why, double limit_s, int code ) {
+    printf( "{\"error\": \"%s\", \"limit_s\": %.1f, \"phase\": %d, \"tiles\": [", why, limit_s, phase.load() );
+    for( int k=0; k<tiles; k++ ) {
+      unsigned long st[6] = { 0 };
+      if( T[k]->a.tile ) fd_verify_tile_state( T[k]->a.tile, st );
+      printf( "%s{\"signal\": %lu, \"open_sigs\": %lu, \"open_age_ns\": %lu, \"inflight\": %lu, \"free\": %lu, "
+              "\"rx\": %lu, \"front_ticket\": %lu, \"produced\": %lu, \"taken\": %lu, \"pub\": %lu}",
+              k ? ", " : "", sig_load( &T[k]->cnc ), st[0], st[1], st[2], st[3], st[4], st[5],
+              T[k]->L.produced.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load() );
+    }
+    printf( "]}\n" );
+    fflush( stdout );
+    fprintf( stderr, "vt_live %s", why );
+    slot_states( shared );
+    fprintf( stderr, "\n" );
+    fflush( stderr );
+    _exit( code );
+  };
+  double const deadline_s = atof( arg( argc, argv, "deadline_s", "0" ) ) > 0. ? atof( arg( argc, argv, "deadline_s", "0" ) )
+                          : ( count ? 0. : seconds ) + 100.;
   std::thread mon( [&]() {
     unsigned long const t0 = now_ns();
     while( !mon_stop.load() ) {
       for( int i=0; i<50 && !mon_stop.load(); i++ ) { struct timespec t = { 0, 100000000L }; nanosleep( &t, NULL ); }
       if( mon_stop.load() ) break;
+      if( (double)( now_ns() - t0 ) * 1e-9 > deadline_s ) stuck_exit( "deadline", deadline_s, 6 );
       fprintf( stderr, "vt_live t=%.1fs phase=%d", (double)( now_ns() - t0 ) * 1e-9, phase.load() );
       for( int k=0; k<tiles; k++ )
         fprintf( stderr, " | tile %d produced=%lu want=%lu taken=%lu pub=%lu signal=%lu", k, T[k]->L.produced.load(),
@@ -558,23 +583,7 @@ int main( int argc, char ** argv ) {
     }
     int stuck = 0;
     for( int k=0; k<tiles; k++ ) stuck |= running[k] && sig_load( &T[k]->cnc ) != FD_VERIFY_TILE_SIGNAL_BOOT;
-    if( stuck ) {
-      printf( "{\"error\": \"halt\", \"halt_s\": %.1f, \"tiles\": [", halt_s );
-      for( int k=0; k<tiles; k++ ) {
-        unsigned long st[6] = { 0 };
-        if( T[k]->a.tile ) fd_verify_tile_state( T[k]->a.tile, st );
-        printf( "%s{\"signal\": %lu, \"open_sigs\": %lu, \"open_age_ns\": %lu, \"inflight\": %lu, \"free\": %lu, "
-                "\"rx\": %lu, \"front_ticket\": %lu, \"produced\": %lu, \"taken\": %lu, \"pub\": %lu}",
-                k ? ", " : "", sig_load( &T[k]->cnc ), st[0], st[1], st[2], st[3], st[4], st[5],
-                T[k]->L.produced.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load() );
-      }
-      printf( "]}\n" );
-      fflush( stdout );
-      slot_states( shared );
-      fprintf( stderr, "\n" );
-      fflush( stderr );
-      _exit( 5 );
-    }
+    if( stuck ) stuck_exit( "halt", halt_s, 5 );
   }
   unsigned long long clk[9] = { 0 };
 #ifndef VT_LIVE_FAKE
