@@ -60,6 +60,8 @@ def main():
             print(json.dumps({"run": i, "mode": mode, "rc": d["rc"], "lat": d["lat"], "dsm_ghz": d.get("dsm_ghz"),
                               "dsm_waves": d.get("dsm_waves"), "batches": d["diag"]["BATCH_CNT"],
                               "age_closes": d["diag"]["AGE_CNT"], "slow": len(slow),
+                              "tile_ns": d.get("tile_ns"), "tile_max_gap_ms": d.get("tile_max_gap_ms"),
+                              "tile_nivcsw": d.get("tile_nivcsw"), "mismatch": d.get("mismatch"),
                               "slow_ranges": [(int(x), int(y), round(float(lat[pub[:, 0] == x][0]), 3)) for x, y in cl[:8]]}),
                   flush=True)
 
