@@ -499,7 +499,7 @@ int main( int argc, char ** argv ) {
     printf( "]}\n" );
     fflush( stdout );
     fprintf( stderr, "vt_live %s", why );
-    slot_states( shared );
+    slot_states( shared ? shared : T[0]->a.gpu );
     fprintf( stderr, "\n" );
     fflush( stderr );
     _exit( code );
@@ -516,7 +516,7 @@ int main( int argc, char ** argv ) {
       for( int k=0; k<tiles; k++ )
         fprintf( stderr, " | tile %d produced=%lu want=%lu taken=%lu pub=%lu signal=%lu", k, T[k]->L.produced.load(),
                  T[k]->L.want_a.load(), T[k]->L.taken_a.load(), T[k]->L.pub_a.load(), sig_load( &T[k]->cnc ) );
-      slot_states( shared );
+      slot_states( shared ? shared : T[0]->a.gpu );
       fprintf( stderr, "\n" );
     }
   } );
